@@ -1,0 +1,299 @@
+"""Generate the golden vectors in tests/golden/*.npz FROM THE REFERENCE ITSELF.
+
+Run only in the build container (where /root/reference exists):
+
+    python tests/golden/gen_golden.py
+
+It imports the reference's own `mx` package (microxscaling/mx) and `funcs`
+approximator API, and restates only the ~30 lines of attention-module glue
+that cannot be imported (the workload modules need timm/diffusers, absent
+here).  The glue follows workloads/deit/scripts/main.py:100-152,
+workloads/DiT/models.py:168-225 and
+workloads/PixArt/models/MX_transformer_block.py:792-859 line for line.
+
+`exponent_based_sign()` raises in funcs/ (SURVEY.md F1), so ex_pred operands
+are taken from partial_K() (Q side) and partial_Q() (K side) of fresh objects
+and cross-checked against the working copy in
+microxscaling/examples/deit/exponent_based_prediction.py.
+
+Nothing from the reference is copied into the repo: only inputs and outputs.
+"""
+import importlib.util
+import os
+import sys
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the reference tree
+
+import numpy as np
+import torch
+
+REF = os.environ.get("MXA_REFERENCE", "/root/reference")
+sys.path.insert(0, os.path.join(REF, "microxscaling"))
+sys.path.insert(0, REF)
+
+import mx  # noqa: E402  (reference)
+from mx.specs import apply_mx_specs  # noqa: E402
+from mx.mx_ops import _quantize_mx, _shared_exponents, _reshape_to_blocks  # noqa: E402
+from mx.elemwise_ops import quantize_elemwise_op  # noqa: E402
+from funcs import exponent_approximation  # noqa: E402  (reference)
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+torch.set_num_threads(8)
+
+BASE_SPECS = {  # workloads/DiT/scripts/sample_ddp.py:51-67 (== deit main.py:716-736)
+    'w_elem_format': 'int8', 'a_elem_format': 'int8', 'scale_bits': 8,
+    'shared_exp_method': 'max', 'block_size': 32, 'bfloat': 32, 'fp': 0,
+    'bfloat_subnorms': True, 'round': 'nearest', 'round_mx_output': 'nearest',
+    'round_output': 'nearest', 'round_weight': 'nearest',
+    'mx_flush_fp32_subnorms': False, 'custom_cuda': False, 'quantize_backprop': False,
+}
+
+
+def specs(**kw):
+    d = dict(BASE_SPECS)
+    d.update(kw)
+    return apply_mx_specs(d)
+
+
+def load_examples_module():
+    path = os.path.join(REF, "microxscaling", "examples", "deit", "exponent_based_prediction.py")
+    spec = importlib.util.spec_from_file_location("examples_ebp", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+EX = load_examples_module()
+
+
+def approx_ops(q, k, s, mode):
+    if mode == "ex_pred":
+        aq = exponent_approximation(Q=q, K=k, mx_specs=s).partial_K()[0]
+        ak = exponent_approximation(Q=q, K=k, mx_specs=s).partial_Q()[1]
+        eq, ek = EX.exponent_approximation(q, k, s).exponent_based_sign()
+        assert torch.equal(eq, aq) and torch.equal(ek, ak), "F2 cross-check failed"
+        return aq, ak
+    if mode == "true_ex":
+        return EX.exponent_approximation(q, k, s).exponent_based_sign_leading_ones()
+    obj = exponent_approximation(Q=q, K=k, mx_specs=s)
+    return getattr(obj, mode)()
+
+
+def attention_glue(q, k, v, s, scale, k_top, mode, top_k=True, approx=True, bias=None):
+    """The mx_quant branch of the patched attention forward (restated)."""
+    res = {}
+    true_scores = mx.matmul(q, k.transpose(-2, -1), mx_specs=s, mode_config='aa')
+    true_scores = true_scores * scale
+    if bias is not None:
+        true_scores += bias
+    res["true"] = true_scores
+    if top_k:
+        if approx:
+            aq, ak = approx_ops(q, k, s, mode)
+            pred = aq @ ak.transpose(-2, -1)
+            if bias is not None:
+                pred = pred + bias
+            res["aq"], res["ak"], res["pred"] = aq, ak, pred
+            _, idx = torch.topk(pred, k_top, dim=-1, largest=True, sorted=True)
+            vals = true_scores.gather(dim=-1, index=idx)
+        else:
+            vals, idx = torch.topk(true_scores, k_top, dim=-1, largest=True, sorted=True)
+        res["idx"], res["vals"] = idx, vals
+        attn = torch.zeros_like(true_scores)
+        attn.scatter_(-1, idx, torch.softmax(vals, dim=-1).to(attn.dtype))
+    else:
+        attn = torch.softmax(true_scores, dim=-1)
+    res["attn"] = attn
+    res["out"] = mx.matmul(attn, v, mx_specs=s, mode_config='aa')
+    # quantized operands of the dense GEMMs (for bit-level checks)
+    from mx.mx_ops import quantize_mx_op  # reference op
+    res["mx_q"] = quantize_mx_op(q, s, elem_format='int8', axes=[-1])
+    res["mx_k"] = quantize_mx_op(k, s, elem_format='int8', axes=[-1])
+    res["mx_v"] = quantize_mx_op(v, s, elem_format='int8', axes=[-2])
+    return {kk: vv.numpy() for kk, vv in res.items()}
+
+
+def rnd(shape, seed, mult=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape, dtype=np.float32) * np.float32(mult)).astype(np.float32)
+
+
+def gen_attention():
+    """One file per input set: inputs, scale and the mode-independent true scores once,
+    then per-variant outputs keyed '<variant>/<name>'."""
+    import math
+
+    def pack(store, tag, r, keep=("pred", "aq", "ak", "idx", "out")):
+        for kk in keep:
+            if kk in r:
+                # approximator operands are pinned on the first 32 rows of every head
+                store[f"{tag}/{kk}"] = r[kk][..., :32, :] if kk in ("aq", "ak") else r[kk]
+
+    # 1 DeiT-tiny single block (configs[0]): B1 H3 N197 d64, k=20; scale = 64**-0.5 (timm)
+    for mult, fname in ((1.0, "attn_deit_tiny"), (3.0, "attn_deit_tiny_peaky")):
+        q, k, v = (torch.from_numpy(rnd((1, 3, 197, 64), s, mult)) for s in (0, 1, 2))
+        sc = 64 ** -0.5
+        store = dict(q=q.numpy(), k=k.numpy(), v=v.numpy(), scale=np.float32(sc))
+        r = attention_glue(q, k, v, specs(), sc, 20, "ex_pred")
+        store.update(true=r["true"], mx_q=r["mx_q"][..., :64, :], mx_k=r["mx_k"][..., :64, :],
+                     mx_v=r["mx_v"][..., :64, :])
+        pack(store, "ex_pred_k20", r)
+        if mult == 1.0:
+            pack(store, "dense", attention_glue(q, k, v, specs(), sc, 20, "ex_pred", top_k=False), ("out",))
+            pack(store, "trueK_k30", attention_glue(q, k, v, specs(), sc, 30, "ex_pred", approx=False),
+                 ("idx", "out"))
+            for mode in ("partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex"):
+                pack(store, f"{mode}_k20", attention_glue(q, k, v, specs(), sc, 20, mode))
+        np.savez_compressed(os.path.join(OUT, fname + ".npz"), **store)
+        print("wrote", fname)
+    # 3 DiT-XL/2 slice: B1 H2 N256 d72, k=154; scale = 72**-0.5 (models.py:130)
+    q, k, v = (torch.from_numpy(rnd((1, 2, 256, 72), s)) for s in (0, 1, 2))
+    sc = 72 ** -0.5
+    r = attention_glue(q, k, v, specs(), sc, 154, "ex_pred")
+    store = dict(q=q.numpy(), k=k.numpy(), v=v.numpy(), scale=np.float32(sc), true=r["true"])
+    pack(store, "ex_pred_k154", r)
+    np.savez_compressed(os.path.join(OUT, "attn_dit.npz"), **store)
+    print("wrote attn_dit")
+    # 5 PixArt cross-attn slice: q (1,2,256,72), k/v (1,2,120,72), 60 valid text tokens,
+    #   bias = (1-mask)*-10000 (MX_pixart_transformer_2d.py:394-397), flush subnormals
+    #   (text_local_inference_alpha.py:121), scale = 1/math.sqrt(72) (MX_transformer_block.py:791)
+    q = torch.from_numpy(rnd((1, 2, 256, 72), 0))
+    k = torch.from_numpy(rnd((1, 2, 120, 72), 1))
+    v = torch.from_numpy(rnd((1, 2, 120, 72), 2))
+    mask = torch.zeros(1, 120)
+    mask[:, :60] = 1
+    bias = ((1 - mask) * -10000.0).unsqueeze(1)  # (B,1,T)
+    attn_bias = torch.zeros([256, 120]) + bias.unsqueeze(1).repeat(1, 2, 1, 1)  # (B,H,N,T)
+    sc = 1 / math.sqrt(72)
+    store = dict(q=q.numpy(), k=k.numpy(), v=v.numpy(), scale=np.float32(sc), bias=bias.numpy())
+    for mode in ("MXINT4", "two_step_leading_ones", "ex_pred"):
+        r = attention_glue(q, k, v, specs(mx_flush_fp32_subnorms=True), sc, 20, mode, bias=attn_bias)
+        store["true"] = r["true"]
+        pack(store, f"{mode}_k20", r)
+    np.savez_compressed(os.path.join(OUT, "attn_pixart_cross.npz"), **store)
+    print("wrote attn_pixart_cross")
+
+
+def gen_quant_kat():
+    """Known-answer + boundary vectors through the reference's _quantize_mx."""
+    out = {}
+    # test_corners_mx.py::test_mx_hw_test inputs (block 10, int8, nearest)
+    hw = np.array([
+        [1.0] * 10, [1.0] * 5 + [2.0] * 5, [-1.0] * 5 + [-2.0] * 5, [1.0] * 5 + [-2.0] * 5,
+        [1.015625, 1.0234375, 1.03125, 1.0390625, 1.25, 1.2578125, 1.9375, 1.9453125, 1.984375, 1.9921875],
+        [-1.984375, -1.9765625, -1.96875, -1.9609375, -1.9375, -1.9296875, -1.75, -1.7421875, -1.0, -1.9921875],
+        [1.99609375, 1.98828125, 0.0, 0.00390625, 0.0078125, 0.01171875, -0.015625, -0.01171875, -0.0078125, -0.00390625],
+    ], dtype=np.float32)
+    out["hw_x"] = hw
+    out["hw_y"] = _quantize_mx(torch.from_numpy(hw), 8, elem_format="int8", block_size=10, axes=1,
+                               round="nearest").numpy()
+    # F5 boundary set + corner blocks, 32-wide rows
+    rng = np.random.default_rng(7)
+    rows = []
+    th = np.load(os.path.join(OUT, "exp_lut.npz"))["th_norm"]
+    for E in range(1, 255):
+        t = int(th[E])
+        for M in sorted({max(0, t - 2), max(0, t - 1), min(t, (1 << 23) - 1), (1 << 23) - 1, 0}):
+            mbits = np.uint32((E << 23) | M)
+            blk = rng.standard_normal(32).astype(np.float32) * np.float32(0.3)
+            blk = np.clip(blk, -0.99, 0.99) * mbits.view(np.float32)
+            blk[rng.integers(32)] = mbits.view(np.float32) * (1 if rng.random() < 0.5 else -1)
+            rows.append(blk.astype(np.float32))
+    sub = np.array([1, 2, 3, 1 << 20, (1 << 23) - 1, (1 << 23) - 40], dtype=np.uint32)
+    for s in sub:
+        blk = np.zeros(32, np.float32)
+        blk[:4] = s.view(np.float32)
+        blk[4:8] = (s // 2).view(np.float32) if s > 1 else 0
+        rows.append(blk)
+    specials = [
+        np.zeros(32, np.float32),
+        np.full(32, 127.0 / 64, np.float32),
+        np.linspace(-1, 1, 32, dtype=np.float32) * np.float32(1.9921875),
+        (np.arange(32, dtype=np.float32) + np.float32(0.5)) / np.float32(64),  # half-way ties
+        np.array([np.float32(3.4028235e38)] + [1.0] * 31, np.float32),
+        np.array([np.inf] + [1.0] * 31, np.float32),
+        np.array([-np.inf] + [1.0] * 31, np.float32),
+        np.array([np.nan] + [1.0] * 31, np.float32),
+        np.array([1e-38, -2e-39] + [0.0] * 30, np.float32),
+    ]
+    rows += specials
+    for _ in range(64):
+        rows.append((rng.standard_normal(32) * np.exp2(rng.integers(-140, 120))).astype(np.float32))
+    X = np.stack(rows).astype(np.float32)
+    out["x"] = X
+    t = torch.from_numpy(X)
+    for elem in ("int8", "int4", "int2"):
+        for rnd_ in ("nearest", "floor", "even"):
+            for flush in (False, True):
+                y = _quantize_mx(t.clone(), 8, elem_format=elem, block_size=32, axes=[-1], round=rnd_,
+                                 flush_fp32_subnorms=flush).numpy()
+                out[f"y_{elem}_{rnd_}_{int(flush)}"] = y
+    out["y_int8_nearest_0_sb5"] = _quantize_mx(t.clone(), 5, elem_format="int8", block_size=32, axes=[-1],
+                                               round="nearest").numpy()
+    # block sizes / axes through the spec-level op
+    Z = rng.standard_normal((3, 70, 45)).astype(np.float32)
+    out["z"] = Z
+    for bs in (8, 9, 32, 64):
+        for ax in (-1, -2, 0):
+            out[f"z_bs{bs}_ax{ax}"] = _quantize_mx(torch.from_numpy(Z), 8, elem_format="int8", block_size=bs,
+                                                   axes=[ax], round="nearest").numpy()
+    # shared exponents (max / none) of the 32-blocks
+    rb, *_ = _reshape_to_blocks(t, [-1], 32)
+    out["sexp_max"] = _shared_exponents(rb, method="max", axes=[-1], ebits=0).numpy()
+    out["sexp_none"] = _shared_exponents(rb, method="none", axes=[-1], ebits=0).numpy()
+    # bfloat16 elementwise (DiT sample.py:42 variant) through quantize_elemwise_op
+    bf = rng.standard_normal(4096).astype(np.float32) * np.exp2(rng.integers(-130, 125, 4096)).astype(np.float32)
+    bf[:8] = [0.0, -0.0, np.inf, -np.inf, 3.3895314e38, 1.1754942e-38, 1e-45, 1.00390625]
+    out["bf_x"] = bf
+    out["bf_y"] = quantize_elemwise_op(torch.from_numpy(bf), specs(bfloat=16), round="nearest").numpy()
+    np.savez_compressed(os.path.join(OUT, "quant_kat.npz"), **out)
+    print("wrote quant_kat", X.shape)
+
+
+def gen_topk_ties():
+    """Tie-heavy ex_pred score rows + torch CPU topk order (pins F3/F4)."""
+    out = {}
+    cfgs = [("deit", (4, 12, 197, 64), (4, 12, 197, 64), 20), ("deit30", (2, 12, 197, 64), (2, 12, 197, 64), 30),
+            ("dit", (2, 4, 256, 72), (2, 4, 256, 72), 154), ("cross", (2, 4, 256, 72), (2, 4, 120, 72), 20)]
+    for name, qs, ks, k in cfgs:
+        q = torch.from_numpy(rnd(qs, 10))
+        kk = torch.from_numpy(rnd(ks, 11))
+        aq, ak = approx_ops(q, kk, specs(), "ex_pred")
+        pred = (aq @ ak.transpose(-2, -1)).reshape(-1, ks[-2])
+        pred = pred[: 1024]
+        _, idx = torch.topk(pred, k, dim=-1, largest=True, sorted=True)
+        out[f"{name}_pred"] = pred.numpy()
+        out[f"{name}_idx"] = idx.numpy().astype(np.int16)
+        out[f"{name}_k"] = np.int64(k)
+    # adversarial rows: constants, few distinct values, sorted, NaN/inf
+    rng = np.random.default_rng(3)
+    adv = []
+    for n in (120, 197, 256):
+        adv.append(np.zeros(n, np.float32))
+        adv.append(np.arange(n, dtype=np.float32))
+        adv.append(np.arange(n, dtype=np.float32)[::-1].copy())
+        for nd in (2, 3, 5):
+            for _ in range(8):
+                adv.append(rng.integers(0, nd, n).astype(np.float32))
+    advs = {}
+    for i, r in enumerate(adv):
+        n = r.shape[0]
+        for k in (1, 2, 3, 20, 30, 77, 154):
+            if k > n:
+                continue
+            _, idx = torch.topk(torch.from_numpy(r), k, largest=True, sorted=True)
+            advs.setdefault(n, []).append((i, k, idx.numpy()))
+    for n, lst in advs.items():
+        rows = np.stack([adv[i] for i, _, _ in lst])
+        ks_ = np.array([k for _, k, _ in lst])
+        idxs = np.full((len(lst), n), -1, np.int16)
+        for j, (_, k, idx) in enumerate(lst):
+            idxs[j, :k] = idx
+        out[f"adv{n}_rows"], out[f"adv{n}_k"], out[f"adv{n}_idx"] = rows, ks_, idxs
+    np.savez_compressed(os.path.join(OUT, "topk_ties.npz"), **out)
+    print("wrote topk_ties")
+
+
+if __name__ == "__main__":
+    gen_quant_kat()
+    gen_topk_ties()
+    gen_attention()

@@ -1,0 +1,164 @@
+"""Pin the CPU oracle (oracle/) against golden vectors generated from the reference.
+
+Bit-exact: MX values / shared exponents, approximator operands, approximate and
+true scores, top-k indices (torch order) and prune masks.  Tolerance (normwise,
+SURVEY.md F7): the attention output.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mx_oracle as O
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(G, name))
+
+
+def same(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if a.dtype.kind == "f":
+        ok = (a == b) | (np.isnan(a) & np.isnan(b))
+        bad = np.argwhere(~ok)
+        assert ok.all(), f"{bad.shape[0]} mismatches, first at {bad[:3].tolist()}: {a[tuple(bad[0])]} vs {b[tuple(bad[0])]}"
+    else:
+        assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- exponent rule
+def test_exp_lut_matches_floor_log2():
+    lut = load("exp_lut.npz")
+    th = lut["th_norm"].astype(np.int64)
+    rng = np.random.default_rng(1)
+    bits = []
+    for E in range(1, 255):
+        t = int(min(th[E], (1 << 23) - 1))
+        lo, hi = max(0, t - 64), min(1 << 23, t + 64)
+        bits.append(np.arange((E << 23) | lo, (E << 23) | hi, dtype=np.uint32))
+        bits.append(((E << 23) | rng.integers(0, 1 << 23, 256)).astype(np.uint32))
+    bits.append(np.arange(1, 1 << 16, dtype=np.uint32))
+    bits.append(np.arange((1 << 23) - 4096, 1 << 23, dtype=np.uint32))
+    b = np.concatenate(bits)
+    E = (b >> 23).astype(np.int64)
+    M = (b & 0x7FFFFF).astype(np.int64)
+    want = np.where(E > 0, E - 127 + (M >= th[E]), 0)
+    sub = E == 0
+    j = np.floor(np.log2(np.maximum(M[sub], 1))).astype(np.int64)
+    want[sub] = -149 + j + (M[sub] >= lut["th_sub"].astype(np.int64)[j])
+    got = O.floor_log2_f32(b.view(np.float32)).astype(np.int64)
+    assert np.array_equal(want, got)
+
+
+def test_exp_rule_vs_torch_sample():
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(2)
+    b = rng.integers(1, 0x7F800000, 1 << 20).astype(np.uint32)
+    x = b.view(np.float32)
+    ref = torch.floor(torch.log2(torch.from_numpy(x))).numpy()
+    same(O.floor_log2_f32(x), ref)
+
+
+# ---------------------------------------------------------------- MX quantize
+def test_hw_kat():
+    d = load("quant_kat.npz")
+    y = O.quantize_mx(d["hw_x"], "int8", 10, 1)[0]
+    same(y, d["hw_y"])
+
+
+@pytest.mark.parametrize("elem", ["int8", "int4", "int2"])
+@pytest.mark.parametrize("rnd", ["nearest", "floor", "even"])
+@pytest.mark.parametrize("flush", [False, True])
+def test_quant_boundary_vectors(elem, rnd, flush):
+    d = load("quant_kat.npz")
+    y = O.quantize_mx(d["x"], elem, 32, -1, 8, rnd, flush)[0]
+    same(y, d[f"y_{elem}_{rnd}_{int(flush)}"])
+
+
+def test_quant_scale_bits5():
+    d = load("quant_kat.npz")
+    same(O.quantize_mx(d["x"], "int8", 32, -1, 5)[0], d["y_int8_nearest_0_sb5"])
+
+
+@pytest.mark.parametrize("bs", [8, 9, 32, 64])
+@pytest.mark.parametrize("ax", [-1, -2, 0])
+def test_quant_block_axis(bs, ax):
+    d = load("quant_kat.npz")
+    same(O.quantize_mx(d["z"], "int8", bs, ax)[0], d[f"z_bs{bs}_ax{ax}"])
+
+
+def test_shared_exponents():
+    d = load("quant_kat.npz")
+    Ab, _ = O.to_blocks(d["x"], -1, 32)
+    same(O.shared_exponents(Ab, "max"), d["sexp_max"])
+    same(O.shared_exponents(Ab, "none"), d["sexp_none"])
+
+
+def test_bfloat16_elemwise():
+    d = load("quant_kat.npz")
+    same(O.quantize_bfloat(d["bf_x"], 16), d["bf_y"])
+
+
+# ---------------------------------------------------------------- top-k order
+@pytest.mark.parametrize("name", ["deit", "deit30", "dit", "cross"])
+def test_topk_ties_exact_order(name):
+    d = load("topk_ties.npz")
+    k = int(d[f"{name}_k"])
+    _, idx = O.topk(d[f"{name}_pred"], k)
+    same(idx.astype(np.int16), d[f"{name}_idx"])
+
+
+@pytest.mark.parametrize("n", [120, 197, 256])
+def test_topk_adversarial(n):
+    d = load("topk_ties.npz")
+    rows, ks, want = d[f"adv{n}_rows"], d[f"adv{n}_k"], d[f"adv{n}_idx"]
+    for r, k, w in zip(rows, ks, want):
+        _, idx = O.topk(r[None], int(k))
+        assert np.array_equal(idx[0].astype(np.int16), w[:k])
+
+
+# ---------------------------------------------------------------- attention
+CASES = [
+    ("attn_deit_tiny.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
+    ("attn_deit_tiny.npz", "dense", dict(top_k=False)),
+    ("attn_deit_tiny.npz", "trueK_k30", dict(approx=False, k_top=30)),
+    ("attn_deit_tiny.npz", "partial_Q_k20", dict(pred_mode="partial_Q", k_top=20)),
+    ("attn_deit_tiny.npz", "partial_K_k20", dict(pred_mode="partial_K", k_top=20)),
+    ("attn_deit_tiny.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20)),
+    ("attn_deit_tiny.npz", "two_step_leading_ones_k20", dict(pred_mode="two_step_leading_ones", k_top=20)),
+    ("attn_deit_tiny.npz", "true_ex_k20", dict(pred_mode="true_ex", k_top=20)),
+    ("attn_deit_tiny_peaky.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
+    ("attn_dit.npz", "ex_pred_k154", dict(pred_mode="ex_pred", k_top=154)),
+    ("attn_pixart_cross.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20, flush=True)),
+    ("attn_pixart_cross.npz", "two_step_leading_ones_k20",
+     dict(pred_mode="two_step_leading_ones", k_top=20, flush=True)),
+    ("attn_pixart_cross.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20, flush=True)),
+]
+
+
+@pytest.mark.parametrize("fname,tag,kw", CASES, ids=[f"{f[5:-4]}:{t}" for f, t, _ in CASES])
+def test_attention_vs_reference(fname, tag, kw):
+    d = load(fname)
+    bias = d["bias"][:, :, None, :] if "bias" in d.files else None
+    r = O.attention(d["q"], d["k"], d["v"], float(d["scale"]), bias=bias, **kw)
+    same(r["true"], d["true"])
+    if f"{tag}/pred" in d.files:
+        same(r["pred"], d[f"{tag}/pred"])
+        same(r["aq"][..., :32, :], d[f"{tag}/aq"])
+        same(r["ak"][..., :32, :], d[f"{tag}/ak"])
+    if f"{tag}/idx" in d.files:
+        same(r["idx"], d[f"{tag}/idx"])
+        T = d["true"].shape[-1]
+        same(O.prune_mask(r["idx"], T), O.prune_mask(d[f"{tag}/idx"], T))
+    err = O.normwise_rel_err(r["out"], d[f"{tag}/out"])
+    # product bar (north star): 1e-3 normwise.  Softmax ulps flip P's MX rounding:
+    # measured 3.9e-4 on the x3 "peaky" input, <=1e-6 elsewhere.
+    assert err <= 1e-3, err
+    if "mx_q" in d.files:
+        same(O.quantize_mx(d["q"], "int8", 32, -1)[0][..., :64, :], d["mx_q"])
+        same(O.quantize_mx(d["k"], "int8", 32, -1)[0][..., :64, :], d["mx_k"])
+        same(O.quantize_mx(d["v"], "int8", 32, -2)[0][..., :64, :], d["mx_v"])
