@@ -297,8 +297,19 @@ def _lib():
         lib.oracle_topk_f32.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_antiqsort.restype = ctypes.c_int
+        lib.oracle_antiqsort.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
         _LIB = lib
     return _LIB
+
+
+def antiqsort_row(n: int, k: int) -> np.ndarray:
+    """A row that exhausts introselect/introsort's depth limit (McIlroy adversary run
+    against libstdc++, oracle/topk_ref.cpp) -- exercises the heap fallbacks."""
+    out = np.zeros(n, dtype=F32)
+    if _lib().oracle_antiqsort(n, k, 1, out.ctypes.data) != 0:
+        raise ValueError("oracle_antiqsort failed")
+    return out
 
 
 def topk(vals: np.ndarray, k: int, largest=True, sorted=True):

@@ -73,3 +73,41 @@ int oracle_topk_f32(const float* vals, int64_t rows, int64_t n, int64_t ld, int6
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Test-input generator: McIlroy's "killer adversary" (A Killer Adversary for
+// Quicksort, 1999) run against the same libstdc++ nth_element + sort that
+// torch's top-k uses.  Produces rows that exhaust introselect's/introsort's
+// depth limit, so the heap_select / heapsort fallbacks get exercised.
+// out[n] receives values such that std::nth_element(.., k-1, .., greater) on
+// them degenerates.
+namespace {
+struct Adversary {
+  std::vector<int64_t> val;
+  int64_t gas, nsolid = 0, candidate = 0;
+  explicit Adversary(int64_t n) : val(n, n), gas(n) {}
+  void freeze(int64_t x) { val[x] = nsolid++; }
+  // "less" on item ids with lazy value assignment
+  bool less(int64_t x, int64_t y) {
+    if (val[x] == gas && val[y] == gas) {
+      if (x == candidate) freeze(x); else freeze(y);
+    }
+    if (val[x] == gas) candidate = x;
+    else if (val[y] == gas) candidate = y;
+    return val[x] < val[y];
+  }
+};
+}  // namespace
+
+extern "C" int oracle_antiqsort(int64_t n, int64_t k, int with_sort, float* out) {
+  if (k < 1 || k > n) return -1;
+  Adversary adv(n);
+  std::vector<int64_t> ids(n);
+  for (int64_t i = 0; i < n; ++i) ids[i] = i;
+  auto cmp = [&](int64_t x, int64_t y) { return adv.less(x, y); };
+  std::nth_element(ids.begin(), ids.begin() + k - 1, ids.end(), cmp);
+  if (with_sort) std::sort(ids.begin(), ids.begin() + k - 1, cmp);
+  // the adversary built an input bad for "less"; negate for torch's "greater"
+  for (int64_t i = 0; i < n; ++i) out[i] = -static_cast<float>(adv.val[i]);
+  return 0;
+}
