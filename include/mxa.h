@@ -1,0 +1,180 @@
+/*
+ * mxa.h -- C ABI of the MI355X-native MX top-k attention library (libmxa.so).
+ *
+ * Plain pointers, sizes and a hipStream_t; no torch types.  Every device
+ * pointer is a gfx950 device allocation; every call is asynchronous on
+ * `stream` and returns an MXA_* status (0 = OK, < 0 = error, nothing launched).
+ * No global state: calls are reentrant; one call per stream at a time.
+ *
+ * Each entry point names the reference interface it replaces.  Reference
+ * paths are relative to d9bjo0522/mx_quantization (snapshot 2025-12-12).
+ * The reference's own native boundary is the pybind module
+ * microxscaling/mx/cpp/funcs.cpp:234-242 (7 functions), JIT-built by
+ * microxscaling/mx/custom_extensions.py:11-19; its Python fallbacks in
+ * mx_ops.py / elemwise_ops.py are what the workloads actually run.
+ */
+#ifndef MXA_H_
+#define MXA_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MXA_ABI_VERSION 1
+
+/* status codes */
+#define MXA_OK 0
+#define MXA_ERR_ARG (-1)          /* bad shape / pointer / option */
+#define MXA_ERR_UNSUPPORTED (-2)  /* valid for the reference, not implemented here */
+#define MXA_ERR_LAUNCH (-3)       /* HIP launch error */
+#define MXA_ERR_WORKSPACE (-4)    /* workspace too small */
+
+/* rounding modes: microxscaling/mx/formats.py:12-16 (RoundingMode) */
+#define MXA_ROUND_NEAREST 0
+#define MXA_ROUND_FLOOR 1
+#define MXA_ROUND_EVEN 2
+
+/* approximator kinds, per operand side.
+ * funcs/exponent_based_prediction.py:44-318 and
+ * microxscaling/examples/deit/exponent_based_prediction.py:135-178 */
+#define MXA_OP_SIGN 0     /* exp-sign:  (mx<0 ? -1 : +1) * 2^e_block        (ex_pred, partial_*) */
+#define MXA_OP_MXINT8 1   /* MXINT8 values                                    (partial_* MX side) */
+#define MXA_OP_MXINT4 2   /* MXINT4 values (Sanger)                           (MXINT4)            */
+#define MXA_OP_EXION 3    /* two_step_leading_ones incl. its e*(...) quirk    (EXION)             */
+#define MXA_OP_TRUE_EX 4  /* exponent_based_sign_leading_ones (values only)   (true_ex)           */
+
+/* prediction modes of the fused op (the caller's `pred_mode`) */
+#define MXA_PRED_EX_PRED 0
+#define MXA_PRED_PARTIAL_Q 1
+#define MXA_PRED_PARTIAL_K 2
+#define MXA_PRED_MXINT4 3
+#define MXA_PRED_EXION 4
+
+int mxa_abi_version(void);
+const char* mxa_status_string(int status);
+
+/*
+ * MX block quantization of a contiguous tensor viewed as (outer, axis_len, inner),
+ * blocks of `block_size` along the middle axis (0 = whole axis), integer element
+ * formats with elem_mbits in {8, 4, 2} (int8 / int4 / int2).
+ * Replaces quantize_mx_op -> _quantize_mx (microxscaling/mx/mx_ops.py:180-341)
+ * and the reference's native quantize_mx_func_cpp / quantize_mx_by_tile_func_cuda
+ * (microxscaling/mx/cpp/funcs.cpp:23-98, :177-231; mx.cu:116-287).
+ *   y      : dequantized values, same layout as x (required)
+ *   codes  : element codes, same layout as x (nullable)
+ *   exps   : block scale exponents (outer, nblocks, inner), INT16_MIN = NaN (nullable)
+ *   bfloat : elementwise pre-rounding of x (0/32 = none, 16 = bfloat16; quantize_elemwise_op)
+ */
+int mxa_quantize_mx(const float* x, float* y, int8_t* codes, int16_t* exps,
+                    int64_t outer, int64_t axis_len, int64_t inner, int32_t block_size,
+                    int32_t elem_mbits, int32_t scale_bits, int32_t round_mode,
+                    int32_t flush_subnormals, int32_t bfloat, hipStream_t stream);
+
+/*
+ * Shared exponents of the blocks of a (outer, axis_len, inner) tensor.
+ * Replaces _shared_exponents (microxscaling/mx/mx_ops.py:49-99).
+ *   method 0 = "max" -> out (outer, nblocks, inner); 1 = "none" -> out like x.
+ *   ebits > 0 applies the [-emax, emax] / NaN clamp of :90-97.
+ */
+int mxa_shared_exponents(const float* x, float* out, int64_t outer, int64_t axis_len, int64_t inner,
+                         int32_t block_size, int32_t method, int32_t ebits, hipStream_t stream);
+
+/*
+ * Elementwise bfloatX quantization.  Replaces quantize_elemwise_op / _quantize_bfloat
+ * (microxscaling/mx/elemwise_ops.py:201-277) and quantize_elemwise_func_cuda
+ * (microxscaling/mx/cpp/elemwise.cu:12-95).
+ */
+int mxa_quantize_bfloat(const float* x, float* y, int64_t n, int32_t bfloat, int32_t round_mode,
+                        int32_t allow_denorm, hipStream_t stream);
+
+/*
+ * Approximator operand values along the last axis (rows x d, leading dims ld_x / ld_out),
+ * MX block size 32.  Replaces the tensors returned by exponent_approximation's methods
+ * (funcs/exponent_based_prediction.py:44-318): op_kind MXA_OP_*.
+ */
+int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64_t ld_x,
+                      int64_t ld_out, int32_t op_kind, int32_t flush_subnormals, int32_t bfloat,
+                      hipStream_t stream);
+
+/*
+ * torch.topk(vals, k, dim=-1, largest=True, sorted=True) with torch's CPU index
+ * order (aten TopKImpl.h:45-86 -> libstdc++ nth_element + sort / partial_sort),
+ * as called at workloads/deit/scripts/main.py:123, workloads/DiT/models.py:194,
+ * workloads/PixArt/models/MX_transformer_block.py:678, :825.
+ * rows x n float32 with leading dim ld; n <= 512.  out_vals nullable.
+ */
+int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
+             int64_t* out_idx, float* out_vals, hipStream_t stream);
+
+/*
+ * The fused hot path: MXINT8 true scores, approximate scores, top-k prune,
+ * softmax over the kept scores, MXINT8 P.V -- the mx_quant branch of
+ *   QuantizedAttention.forward  workloads/deit/scripts/main.py:100-152
+ *   Attention.forward           workloads/DiT/models.py:168-225
+ *   MXSelfAttention.forward     workloads/PixArt/models/MX_transformer_block.py:648-717
+ *   MXCrossAttention.forward    workloads/PixArt/models/MX_transformer_block.py:792-859
+ * from q (B,H,N,D), k/v (B,H,T,D) to the pre-projection output (B,H,N,D).
+ * Strides are in elements for the (b,h,row) dims; the D dim must be contiguous.
+ */
+typedef struct mxa_attn_params {
+  const float* q;
+  const float* k;
+  const float* v;
+  int64_t q_strides[3];
+  int64_t k_strides[3];
+  int64_t v_strides[3];
+  int32_t B, H, N, T, D;
+  int32_t k_top;           /* kept keys per query row (top_k != 0)                         */
+  float scale;             /* float32(head_dim ** -0.5) as the caller computes it          */
+  int32_t pred_mode;       /* MXA_PRED_*                                                   */
+  int32_t top_k;           /* 0: dense softmax (blocks excluded from top-k)                */
+  int32_t approx;          /* 0: top-k on the true scores (approx_flag / ex_pred False)    */
+  int32_t flush_subnormals;/* mx_specs["mx_flush_fp32_subnorms"]                           */
+  int32_t bfloat;          /* mx_specs["bfloat"]: 0/32 none, 16 bfloat16                   */
+  const float* bias;       /* additive score bias (PixArt mask), nullable                 */
+  int64_t bias_strides[4]; /* (b,h,n,t) element strides, 0 = broadcast                     */
+  float* out;              /* (B,H,N,D) output                                             */
+  int64_t out_strides[3];
+  int64_t* idx_out;        /* (B,H,N,k_top) contiguous int64, nullable                     */
+  float* true_out;         /* optional (B,H,N,T) contiguous true scores (tests)            */
+  float* pred_out;         /* optional (B,H,N,T) contiguous approximate scores (tests)    */
+  void* workspace;         /* device scratch of mxa_attention_workspace_bytes() bytes     */
+  int64_t workspace_bytes;
+} mxa_attn_params;
+
+int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p);
+int mxa_attention(const mxa_attn_params* p, hipStream_t stream);
+
+/*
+ * Measurement entry point (bench.py): runs mxa_attention `iters` times on `stream`
+ * recording HIP events between the kernels, synchronizes the stream, and writes
+ * the mean milliseconds of each stage to stage_ms[MXA_ATTN_STAGES]:
+ *   0 rows_prep(Q)  1 rows_prep(K)  2 cols_prep(V)  3 scores+top-k+softmax+P-quant  4 P.V
+ * Host-synchronizing: not for use inside graph capture.
+ */
+#define MXA_ATTN_STAGES 5
+#define MXA_ATTN_STAGES_PLUS1 6
+int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms);
+
+/*
+ * mx.matmul forward (microxscaling/mx/matmul.py:31-100, :211-222): in1 (batch, M, K)
+ * quantized along K, in2 (batch, K, Nc) quantized along K, fp32 result (batch, M, Nc)
+ * contiguous.  Integer formats, block size 32.
+ */
+int mxa_matmul(const float* a, const float* b, float* c, int64_t batch, int32_t M, int32_t K,
+               int32_t Nc, int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a,
+               int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, void* workspace,
+               int64_t workspace_bytes, hipStream_t stream);
+int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc);
+
+/* Self-test of the int8 MFMA operand/accumulator lane maps (16x16x32): writes
+ * C = A(16x32) * B(32x16) computed by MFMA and returns MXA_OK; host compares. */
+int mxa_selftest_mfma(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MXA_H_ */

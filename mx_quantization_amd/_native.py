@@ -1,0 +1,112 @@
+"""ctypes binding of libmxa.so (the C ABI declared in include/mxa.h).
+
+torch is imported first on purpose: libmxa.so needs libamdhip64.so.7, and the
+dynamic loader then binds it to the runtime torch already loaded, so torch's
+streams and device pointers are valid inside the library.
+
+There is no fallback: if the library is missing or fails to load, every op
+raises.  Build it with `python -m mx_quantization_amd.build_native`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading libmxa.so, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmxa.so")
+
+c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+MXA_OK = 0
+MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
+PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4}
+ROUND_MODES = {"nearest": 0, "floor": 1, "even": 2}
+
+
+class AttnParams(ctypes.Structure):
+    """mirror of struct mxa_attn_params (include/mxa.h)"""
+    _fields_ = [
+        ("q", c_vp), ("k", c_vp), ("v", c_vp),
+        ("q_strides", c_i64 * 3), ("k_strides", c_i64 * 3), ("v_strides", c_i64 * 3),
+        ("B", c_i32), ("H", c_i32), ("N", c_i32), ("T", c_i32), ("D", c_i32),
+        ("k_top", c_i32), ("scale", c_f32), ("pred_mode", c_i32), ("top_k", c_i32), ("approx", c_i32),
+        ("flush_subnormals", c_i32), ("bfloat", c_i32),
+        ("bias", c_vp), ("bias_strides", c_i64 * 4),
+        ("out", c_vp), ("out_strides", c_i64 * 3),
+        ("idx_out", c_vp), ("true_out", c_vp), ("pred_out", c_vp),
+        ("workspace", c_vp), ("workspace_bytes", c_i64),
+    ]
+
+
+_SIGS = {
+    "mxa_abi_version": (c_i32, []),
+    "mxa_status_string": (ctypes.c_char_p, [c_i32]),
+    "mxa_quantize_mx": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                c_i32, c_vp]),
+    "mxa_shared_exponents": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_quantize_bfloat": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_approx_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "mxa_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams)]),
+    "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
+    "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
+    "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
+                           c_vp, c_i64, c_vp]),
+    "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
+    "mxa_selftest_mfma": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """The loaded library (raises NativeError when absent -- no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} is missing: build it with `python -m mx_quantization_amd.build_native`")
+        try:
+            handle = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.mxa_abi_version() != 1:
+            raise NativeError("libmxa.so ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != MXA_OK:
+        msg = lib().mxa_status_string(status).decode()
+        raise NativeError(f"{what} failed: {msg} (status {status})")
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors: torch.Tensor) -> torch.device:
+    """The product path runs on the MI355X only; CPU tensors are an error, not a fallback."""
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise NativeError("mx_quantization_amd ops run on a HIP device; got a CPU tensor "
+                              "(the CPU restatement lives in oracle/ and is test infrastructure only)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise NativeError("tensors on different devices")
+    return dev

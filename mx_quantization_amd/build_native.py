@@ -1,0 +1,55 @@
+"""Build libmxa.so (the HIP kernels + C ABI of include/mxa.h) for gfx950, in-tree.
+
+    python -m mx_quantization_amd.build_native      (or __graft_entry__.build())
+
+hipcc cross-compiles without a GPU.  The library links the HIP runtime by
+SONAME (libamdhip64.so.7); when torch is imported first the process reuses
+torch's runtime, so torch streams and device pointers are valid in it.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libmxa.so")
+SOURCES = ["mxa_quant.hip", "mxa_attn.hip"]
+HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_topk.hpp", "mxa_exp_lut.h", "../../include/mxa.h"]
+ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    if not force and not _stale():
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+               "-Wall", "-Wno-unused-function", "-I", os.path.join(HERE, "..", "include"),
+               "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB)

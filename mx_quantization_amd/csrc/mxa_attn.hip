@@ -1,0 +1,597 @@
+// The MX top-k attention hot path on gfx950.
+//
+//   rows_prep(Q), rows_prep(K)  MXINT8 codes + block exponents + approximator operands
+//   cols_prep(V)                MXINT8 codes of V along tokens, stored [d][t]
+//   scores_topk_kernel          per (head, 16 query rows): true + approximate scores on
+//                               int8 MFMA with exact block epilogues, wave-per-row top-k
+//                               in torch's CPU order, softmax over the kept scores,
+//                               scatter, MX quantization of P along keys
+//   pv_kernel                   P.V on int8 MFMA (per-block scales 2^(eP + eV))
+//
+// This is the mx_quant branch of the patched attention forward:
+//   workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
+//   workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859.
+#include "mxa_kernels.hpp"
+#include "mxa_topk.hpp"
+
+#include <vector>
+
+namespace mxa {
+
+constexpr int kRowsPerWG = 16;
+
+struct ScoresArgs {
+  const int8_t *qc, *qop, *kc, *kop;
+  const int16_t *qsT, *qsA, *ksT, *ksA;
+  int B, H, N, T, nbd, dpad, ntb, tpad;
+  int k_top, top_k, approx, mul_combine, bfloat, flush_p;
+  float scale;
+  const float* bias;
+  int64_t bs0, bs1, bs2, bs3;
+  int64_t* idx_out;
+  float* true_out;
+  float* pred_out;
+  int8_t* pc;   // [B*H*N][tpad]
+  int16_t* ps;  // [B*H*N][ntb]
+};
+
+template <int S>
+__global__ __launch_bounds__(256) void scores_topk_kernel(ScoresArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* tileT = reinterpret_cast<float*>(smem);   // [16][tpad] true scores (then P)
+  float* tileP = tileT + kRowsPerWG * a.tpad;       // [16][tpad] approximate scores
+  uint64_t* scr_base = reinterpret_cast<uint64_t*>(tileP + kRowsPerWG * a.tpad);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.y;
+  const int row0 = blockIdx.x * kRowsPerWG;
+  const int rows_valid = min(kRowsPerWG, a.N - row0);
+  const int b = bh / a.H, h = bh % a.H;
+  const bool need_pred = a.top_k && a.approx;
+
+  // ---- block-scaled int8 MFMA scores for 16 rows x T columns ----------------
+  const int64_t qrow0 = (int64_t)bh * a.N + row0;
+  const int64_t krow0 = (int64_t)bh * a.T;
+  const int ntiles = (a.T + 15) / 16;
+  for (int ct = wave; ct < ntiles; ct += 4) {
+    const int col0 = ct * 16;
+    const int cols_valid = min(16, a.T - col0);
+    double accT[4] = {0.0, 0.0, 0.0, 0.0};
+    double accP[4] = {0.0, 0.0, 0.0, 0.0};
+    scaled_tile<false>(a.qc + qrow0 * a.dpad, a.dpad, rows_valid, a.qsT + qrow0 * a.nbd, a.nbd, 1,
+                       a.kc + (krow0 + col0) * a.dpad, a.dpad, cols_valid, a.ksT + (krow0 + col0) * a.nbd,
+                       a.nbd, 1, a.nbd, accT);
+    if (need_pred) {
+      if (a.mul_combine)
+        scaled_tile<true>(a.qop + qrow0 * a.dpad, a.dpad, rows_valid, a.qsA + qrow0 * a.nbd, a.nbd, 1,
+                          a.kop + (krow0 + col0) * a.dpad, a.dpad, cols_valid, a.ksA + (krow0 + col0) * a.nbd,
+                          a.nbd, 1, a.nbd, accP);
+      else
+        scaled_tile<false>(a.qop + qrow0 * a.dpad, a.dpad, rows_valid, a.qsA + qrow0 * a.nbd, a.nbd, 1,
+                           a.kop + (krow0 + col0) * a.dpad, a.dpad, cols_valid, a.ksA + (krow0 + col0) * a.nbd,
+                           a.nbd, 1, a.nbd, accP);
+    }
+    const int col = col0 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (lane >> 4) + i;
+      if (r < rows_valid && col < a.T) {
+        // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)   (matmul.py:88-91, caller)
+        float t = round_bfloat((float)accT[i], a.bfloat, kRoundNearest, 1);
+        t = t * a.scale;
+        float bv = 0.0f;
+        if (a.bias) {
+          bv = a.bias[b * a.bs0 + h * a.bs1 + (int64_t)(row0 + r) * a.bs2 + (int64_t)col * a.bs3];
+          t = t + bv;
+        }
+        tileT[r * a.tpad + col] = t;
+        const int64_t go = (qrow0 + r) * a.T + col;
+        if (a.true_out) a.true_out[go] = t;
+        if (need_pred) {
+          float p = (float)accP[i];
+          if (a.bias) p = p + bv;
+          tileP[r * a.tpad + col] = p;
+          if (a.pred_out) a.pred_out[go] = p;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- per row: top-k, softmax, scatter, MX-quantize P along keys ----------
+  TopkLds sc;
+  sc.a = scr_base + (size_t)wave * 2 * (64 * S);
+  sc.b = sc.a + 64 * S;
+  for (int r = wave; r < rows_valid; r += 4) {
+    const int64_t grow = qrow0 + r;
+    float* trow = tileT + r * a.tpad;
+    float* prow = tileP + r * a.tpad;
+    float pv[S];
+    if (a.top_k) {
+      WaveRow<S> w;
+      w.lane = lane;
+      const float* src = a.approx ? prow : trow;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        w.key[s] = pos < a.T ? order_key(src[pos]) : 0u;
+        w.idx[s] = (uint32_t)pos;
+      }
+      wave_topk<S>(w, a.T, a.k_top, sc);
+      // vals = true.gather(idx); softmax(vals); zeros.scatter_(idx, softmax)
+      float v[S];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        v[s] = -INFINITY;
+        if (pos < a.k_top) {
+          if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)w.idx[s];
+          v[s] = trow[w.idx[s]];
+          mx = fmaxf(mx, v[s]);
+        }
+      }
+      mx = wave_max_f32(mx);
+      float sum = 0.0f;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        v[s] = pos < a.k_top ? expf(v[s] - mx) : 0.0f;
+        sum += v[s];
+      }
+      sum = wave_sum_f32(sum);
+      wave_lds_sync();
+      for (int pos = lane; pos < a.tpad; pos += 64) prow[pos] = 0.0f;
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        if (pos < a.k_top) prow[w.idx[s]] = v[s] / sum;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        pv[s] = pos < a.tpad ? prow[pos] : 0.0f;
+      }
+    } else {
+      // dense: attn = softmax(true) (blocks excluded from top-k)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        pv[s] = pos < a.T ? trow[pos] : -INFINITY;
+        mx = fmaxf(mx, pv[s]);
+      }
+      mx = wave_max_f32(mx);
+      float sum = 0.0f;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        pv[s] = pos < a.T ? expf(pv[s] - mx) : 0.0f;
+        sum += pv[s];
+      }
+      sum = wave_sum_f32(sum);
+#pragma unroll
+      for (int s = 0; s < S; ++s) pv[s] = pv[s] / sum;
+    }
+    // P -> MXINT8 along keys (matmul(attn, v): quantize_mx_op(axes=[-1]), matmul.py:68-76)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      if (s * 64 >= a.tpad) break;
+      const float x = round_bfloat(pv[s], a.bfloat, kRoundNearest, 1);
+      uint32_t mb = __float_as_uint(x) & 0x7FFFFFFFu;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t w2 = (uint32_t)__shfl_xor((int)mb, o, 32);
+        mb = w2 > mb ? w2 : mb;
+      }
+      int e_raw;
+      const int es = scale_exponent(mb, 127, &e_raw);
+      float xv = x;
+      if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
+      const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+      if (pos < a.tpad) {
+        a.pc[grow * a.tpad + pos] = (int8_t)code;
+        if ((lane & 31) == 0) a.ps[grow * a.ntb + (pos >> 5)] = exp_to16(es == kExpNaN ? kExpNaN : es - 6);
+      }
+    }
+  }
+}
+
+struct PVArgs {
+  const int8_t* pc;
+  const int16_t* ps;
+  const int8_t* vt;
+  const int16_t* vs;
+  int B, H, N, D, ntb, tpad, bfloat;
+  float* out;
+  int64_t os0, os1, os2;
+};
+
+__global__ __launch_bounds__(256) void pv_kernel(PVArgs a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.y;
+  const int row0 = blockIdx.x * kRowsPerWG;
+  const int rows_valid = min(kRowsPerWG, a.N - row0);
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t prow0 = (int64_t)bh * a.N + row0;
+  const int ntiles = (a.D + 15) / 16;
+  for (int ct = wave; ct < ntiles; ct += 4) {
+    const int col0 = ct * 16;
+    const int cols_valid = min(16, a.D - col0);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    scaled_tile<false>(a.pc + prow0 * a.tpad, a.tpad, rows_valid, a.ps + prow0 * a.ntb, a.ntb, 1,
+                       a.vt + ((int64_t)bh * a.D + col0) * a.tpad, a.tpad, cols_valid,
+                       a.vs + (int64_t)bh * a.ntb * a.D + col0, 1, a.D, a.ntb, acc);
+    const int col = col0 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (lane >> 4) + i;
+      if (r < rows_valid && col < a.D)
+        a.out[b * a.os0 + h * a.os1 + (int64_t)(row0 + r) * a.os2 + col] =
+            round_bfloat((float)acc[i], a.bfloat, kRoundNearest, 1);
+    }
+  }
+}
+
+// ---- standalone exact-order top-k over rows of a float matrix --------------
+struct TopkArgs {
+  const float* vals;
+  int64_t rows, ld;
+  int n, k;
+  int64_t* out_idx;
+  float* out_vals;
+};
+
+template <int S>
+__global__ __launch_bounds__(256) void topk_rows_kernel(TopkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= a.rows) return;  // wave-uniform
+  TopkLds sc;
+  sc.a = reinterpret_cast<uint64_t*>(smem) + (size_t)wave * 2 * (64 * S);
+  sc.b = sc.a + 64 * S;
+  const float* src = a.vals + row * a.ld;
+  WaveRow<S> w;
+  w.lane = lane;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = s * 64 + lane;
+    w.key[s] = pos < a.n ? order_key(src[pos]) : 0u;
+    w.idx[s] = (uint32_t)pos;
+  }
+  wave_topk<S>(w, a.n, a.k, sc);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = s * 64 + lane;
+    if (pos < a.k) {
+      a.out_idx[row * a.k + pos] = (int64_t)w.idx[s];
+      if (a.out_vals) a.out_vals[row * a.k + pos] = src[w.idx[s]];
+    }
+  }
+}
+
+// ---- mx.matmul: C[b] = MX(A[b], along K) @ MX(B[b], along K) ---------------
+struct MatmulArgs {
+  const int8_t* ac;
+  const int16_t* as;
+  const int8_t* bt;
+  const int16_t* bsc;
+  int M, Nc, nbk, kpad, bfloat;
+  float* c;
+};
+
+__global__ __launch_bounds__(256) void matmul_kernel(MatmulArgs a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t bt = blockIdx.z;
+  const int row0 = blockIdx.y * 16;
+  const int col0 = (blockIdx.x * 4 + wave) * 16;
+  if (col0 >= a.Nc) return;
+  const int rows_valid = min(16, a.M - row0);
+  const int cols_valid = min(16, a.Nc - col0);
+  const int64_t arow0 = bt * a.M + row0;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  scaled_tile<false>(a.ac + arow0 * a.kpad, a.kpad, rows_valid, a.as + arow0 * a.nbk, a.nbk, 1,
+                     a.bt + (bt * a.Nc + col0) * a.kpad, a.kpad, cols_valid, a.bsc + bt * a.nbk * a.Nc + col0,
+                     1, a.Nc, a.nbk, acc);
+  const int col = col0 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * (lane >> 4) + i;
+    if (r < rows_valid && col < a.Nc)
+      a.c[(arow0 + r) * a.Nc + col] = round_bfloat((float)acc[i], a.bfloat, kRoundNearest, 1);
+  }
+}
+
+__global__ void selftest_mfma_kernel(const int8_t* A, const int8_t* B, int32_t* C) {
+  // A row-major 16x32, B row-major 32x16 (k-major), C row-major 16x16
+  const int lane = threadIdx.x;
+  const int r = lane & 15, kg = lane >> 4;
+  long av = 0, bv = 0;
+  for (int j = 0; j < 8; ++j) {
+    av |= (long)(uint8_t)A[r * 32 + kg * 8 + j] << (8 * j);
+    bv |= (long)(uint8_t)B[(kg * 8 + j) * 16 + r] << (8 * j);
+  }
+  const v4i zero = {0, 0, 0, 0};
+  const v4i c = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, zero, 0, 0, 0);
+  for (int i = 0; i < 4; ++i) C[(4 * kg + i) * 16 + r] = c[i];
+}
+
+}  // namespace mxa
+
+using namespace mxa;
+
+namespace {
+
+constexpr int64_t kAlign = 256;
+inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+struct AttnLayout {
+  int nbd, dpad, ntb, tpad;
+  int64_t qc, qop, qsT, qsA, kc, kop, ksT, ksA, vt, vs, pc, ps, total;
+};
+
+AttnLayout attn_layout(const mxa_attn_params* p) {
+  AttnLayout L{};
+  const int64_t BH = (int64_t)p->B * p->H;
+  L.nbd = (p->D + 31) / 32;
+  L.dpad = L.nbd * 32;
+  L.ntb = (p->T + 31) / 32;
+  L.tpad = L.ntb * 32;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  const int64_t qrows = BH * p->N, krows = BH * p->T;
+  L.qc = take(qrows * L.dpad);
+  L.qop = take(qrows * L.dpad);
+  L.qsT = take(qrows * L.nbd * 2);
+  L.qsA = take(qrows * L.nbd * 2);
+  L.kc = take(krows * L.dpad);
+  L.kop = take(krows * L.dpad);
+  L.ksT = take(krows * L.nbd * 2);
+  L.ksA = take(krows * L.nbd * 2);
+  L.vt = take(BH * p->D * (int64_t)L.tpad);
+  L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
+  L.pc = take(qrows * L.tpad);
+  L.ps = take(qrows * L.ntb * 2);
+  L.total = off;
+  return L;
+}
+
+bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int mxa_abi_version(void) { return MXA_ABI_VERSION; }
+
+extern "C" const char* mxa_status_string(int status) {
+  switch (status) {
+    case MXA_OK: return "ok";
+    case MXA_ERR_ARG: return "invalid argument";
+    case MXA_ERR_UNSUPPORTED: return "unsupported configuration";
+    case MXA_ERR_LAUNCH: return "HIP kernel launch failed";
+    case MXA_ERR_WORKSPACE: return "workspace too small";
+    default: return "unknown status";
+  }
+}
+
+extern "C" int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p) {
+  if (!p || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return -1;
+  return attn_layout(p).total;
+}
+
+template <int S>
+static int launch_scores(const ScoresArgs& sa, int BH, int N, hipStream_t stream) {
+  const size_t lds = (size_t)2 * kRowsPerWG * sa.tpad * sizeof(float) + (size_t)4 * 2 * 64 * S * sizeof(uint64_t);
+  dim3 grid((unsigned)((N + kRowsPerWG - 1) / kRowsPerWG), (unsigned)BH);
+  if (lds > 65536 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&scores_topk_kernel<S>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL(scores_topk_kernel<S>, grid, dim3(256), lds, stream, sa);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev) {
+  if (!p || !p->q || !p->k || !p->v || !p->out) return MXA_ERR_ARG;
+  if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
+  if (p->T > 512) return MXA_ERR_UNSUPPORTED;
+  if (p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
+  if (p->pred_mode < MXA_PRED_EX_PRED || p->pred_mode > MXA_PRED_EXION) return MXA_ERR_ARG;
+  if (p->bfloat != 0 && p->bfloat != 32 && (p->bfloat < 10 || p->bfloat > 31)) return MXA_ERR_ARG;
+  const AttnLayout L = attn_layout(p);
+  if (!p->workspace || p->workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
+  unsigned char* ws = static_cast<unsigned char*>(p->workspace);
+  if (!aligned16(ws)) return MXA_ERR_ARG;
+  const int64_t BH = (int64_t)p->B * p->H;
+
+  int opq = MXA_OP_SIGN, opk = MXA_OP_SIGN;
+  switch (p->pred_mode) {
+    case MXA_PRED_PARTIAL_Q: opq = MXA_OP_MXINT8; break;  // Q = MXINT8, K = exp-sign
+    case MXA_PRED_PARTIAL_K: opk = MXA_OP_MXINT8; break;  // Q = exp-sign, K = MXINT8
+    case MXA_PRED_MXINT4: opq = opk = MXA_OP_MXINT4; break;
+    case MXA_PRED_EXION: opq = opk = MXA_OP_EXION; break;
+    default: break;
+  }
+  const bool need_pred = p->top_k && p->approx;
+
+  RowsPrepArgs rq{};
+  rq.x = p->q; rq.s0 = p->q_strides[0]; rq.s1 = p->q_strides[1]; rq.s2 = p->q_strides[2];
+  rq.H = p->H; rq.R = p->N; rq.rows = BH * p->N; rq.D = p->D; rq.nb = L.nbd; rq.dpad = L.dpad;
+  rq.vec4 = aligned16(p->q) && (p->q_strides[0] % 4 == 0) && (p->q_strides[1] % 4 == 0) && (p->q_strides[2] % 4 == 0);
+  rq.op_kind = opq; rq.flush = p->flush_subnormals; rq.bfloat = p->bfloat;
+  rq.codes = reinterpret_cast<int8_t*>(ws + L.qc);
+  rq.sT = reinterpret_cast<int16_t*>(ws + L.qsT);
+  rq.op = need_pred ? reinterpret_cast<int8_t*>(ws + L.qop) : nullptr;
+  rq.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  int rc = launch_rows_prep(rq, stream);
+  if (rc) return rc;
+  if (ev) (void)hipEventRecord(ev[1], stream);
+
+  RowsPrepArgs rk = rq;
+  rk.x = p->k; rk.s0 = p->k_strides[0]; rk.s1 = p->k_strides[1]; rk.s2 = p->k_strides[2];
+  rk.R = p->T; rk.rows = BH * p->T;
+  rk.vec4 = aligned16(p->k) && (p->k_strides[0] % 4 == 0) && (p->k_strides[1] % 4 == 0) && (p->k_strides[2] % 4 == 0);
+  rk.op_kind = opk;
+  rk.codes = reinterpret_cast<int8_t*>(ws + L.kc);
+  rk.sT = reinterpret_cast<int16_t*>(ws + L.ksT);
+  rk.op = need_pred ? reinterpret_cast<int8_t*>(ws + L.kop) : nullptr;
+  rk.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.ksA) : nullptr;
+  rc = launch_rows_prep(rk, stream);
+  if (rc) return rc;
+  if (ev) (void)hipEventRecord(ev[2], stream);
+
+  ColsPrepArgs cv{};
+  cv.x = p->v; cv.s0 = p->v_strides[0]; cv.s1 = p->v_strides[1]; cv.s2 = p->v_strides[2];
+  cv.H = p->H; cv.mats = BH; cv.R = p->T; cv.C = p->D; cv.nb = L.ntb; cv.rpad = L.tpad;
+  cv.mbits = 8; cv.flush = p->flush_subnormals; cv.bfloat = p->bfloat;
+  cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
+  cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
+  rc = launch_cols_prep(cv, stream);
+  if (rc) return rc;
+  if (ev) (void)hipEventRecord(ev[3], stream);
+
+  ScoresArgs sa{};
+  sa.qc = reinterpret_cast<const int8_t*>(ws + L.qc);
+  sa.qop = reinterpret_cast<const int8_t*>(ws + L.qop);
+  sa.kc = reinterpret_cast<const int8_t*>(ws + L.kc);
+  sa.kop = reinterpret_cast<const int8_t*>(ws + L.kop);
+  sa.qsT = reinterpret_cast<const int16_t*>(ws + L.qsT);
+  sa.qsA = reinterpret_cast<const int16_t*>(ws + L.qsA);
+  sa.ksT = reinterpret_cast<const int16_t*>(ws + L.ksT);
+  sa.ksA = reinterpret_cast<const int16_t*>(ws + L.ksA);
+  sa.B = p->B; sa.H = p->H; sa.N = p->N; sa.T = p->T;
+  sa.nbd = L.nbd; sa.dpad = L.dpad; sa.ntb = L.ntb; sa.tpad = L.tpad;
+  sa.k_top = p->k_top; sa.top_k = p->top_k; sa.approx = p->approx;
+  sa.mul_combine = p->pred_mode == MXA_PRED_EXION;
+  sa.bfloat = p->bfloat; sa.flush_p = p->flush_subnormals;
+  sa.scale = p->scale;
+  sa.bias = p->bias;
+  sa.bs0 = p->bias_strides[0]; sa.bs1 = p->bias_strides[1]; sa.bs2 = p->bias_strides[2]; sa.bs3 = p->bias_strides[3];
+  sa.idx_out = p->idx_out; sa.true_out = p->true_out; sa.pred_out = p->pred_out;
+  sa.pc = reinterpret_cast<int8_t*>(ws + L.pc);
+  sa.ps = reinterpret_cast<int16_t*>(ws + L.ps);
+  const int S = (p->T + 63) / 64;
+  if (S <= 1) rc = launch_scores<1>(sa, (int)BH, p->N, stream);
+  else if (S <= 2) rc = launch_scores<2>(sa, (int)BH, p->N, stream);
+  else if (S <= 4) rc = launch_scores<4>(sa, (int)BH, p->N, stream);
+  else rc = launch_scores<8>(sa, (int)BH, p->N, stream);
+  if (rc) return rc;
+  if (ev) (void)hipEventRecord(ev[4], stream);
+
+  PVArgs pa{};
+  pa.pc = sa.pc; pa.ps = sa.ps;
+  pa.vt = reinterpret_cast<const int8_t*>(ws + L.vt);
+  pa.vs = reinterpret_cast<const int16_t*>(ws + L.vs);
+  pa.B = p->B; pa.H = p->H; pa.N = p->N; pa.D = p->D; pa.ntb = L.ntb; pa.tpad = L.tpad; pa.bfloat = p->bfloat;
+  pa.out = p->out; pa.os0 = p->out_strides[0]; pa.os1 = p->out_strides[1]; pa.os2 = p->out_strides[2];
+  dim3 grid((unsigned)((p->N + kRowsPerWG - 1) / kRowsPerWG), (unsigned)BH);
+  hipLaunchKernelGGL(pv_kernel, grid, dim3(256), 0, stream, pa);
+  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  if (ev) (void)hipEventRecord(ev[5], stream);
+  return MXA_OK;
+}
+
+extern "C" int mxa_attention(const mxa_attn_params* p, hipStream_t stream) {
+  return attention_impl(p, stream, nullptr);
+}
+
+extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms) {
+  if (iters <= 0 || !stage_ms) return MXA_ERR_ARG;
+  std::vector<hipEvent_t> ev((size_t)iters * MXA_ATTN_STAGES_PLUS1);
+  for (auto& e : ev)
+    if (hipEventCreate(&e) != hipSuccess) return MXA_ERR_LAUNCH;
+  int rc = MXA_OK;
+  for (int i = 0; i < iters && rc == MXA_OK; ++i) rc = attention_impl(p, stream, &ev[(size_t)i * MXA_ATTN_STAGES_PLUS1]);
+  if (rc == MXA_OK && hipStreamSynchronize(stream) != hipSuccess) rc = MXA_ERR_LAUNCH;
+  if (rc == MXA_OK) {
+    for (int s = 0; s < MXA_ATTN_STAGES; ++s) {
+      double acc = 0.0;
+      for (int i = 0; i < iters; ++i) {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, ev[(size_t)i * MXA_ATTN_STAGES_PLUS1 + s], ev[(size_t)i * MXA_ATTN_STAGES_PLUS1 + s + 1]);
+        acc += ms;
+      }
+      stage_ms[s] = (float)(acc / iters);
+    }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc;
+}
+
+template <int S>
+static int launch_topk(const TopkArgs& ta, hipStream_t stream) {
+  const size_t lds = (size_t)4 * 2 * 64 * S * sizeof(uint64_t);
+  hipLaunchKernelGGL(topk_rows_kernel<S>, dim3((unsigned)((ta.rows + 3) / 4)), dim3(256), lds, stream, ta);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
+                        float* out_vals, hipStream_t stream) {
+  if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
+  if (n > 512) return MXA_ERR_UNSUPPORTED;
+  if (rows == 0 || k == 0) return MXA_OK;
+  TopkArgs ta{vals, rows, ld, n, k, out_idx, out_vals};
+  const int S = (n + 63) / 64;
+  if (S <= 1) return launch_topk<1>(ta, stream);
+  if (S <= 2) return launch_topk<2>(ta, stream);
+  if (S <= 4) return launch_topk<4>(ta, stream);
+  return launch_topk<8>(ta, stream);
+}
+
+extern "C" int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc) {
+  if (batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return -1;
+  const int64_t nbk = (K + 31) / 32, kpad = nbk * 32;
+  return align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) + align_up(batch * Nc * kpad) +
+         align_up(batch * nbk * Nc * 2);
+}
+
+extern "C" int mxa_matmul(const float* a, const float* b, float* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
+                          int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a, int32_t elem_mbits_b,
+                          int32_t flush_subnormals, int32_t bfloat, void* workspace, int64_t workspace_bytes,
+                          hipStream_t stream) {
+  if (!a || !b || !c || batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return MXA_ERR_ARG;
+  if ((elem_mbits_a != 8 && elem_mbits_a != 4) || (elem_mbits_b != 8 && elem_mbits_b != 4))
+    return MXA_ERR_UNSUPPORTED;
+  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
+  const int64_t need = mxa_matmul_workspace_bytes(batch, M, K, Nc);
+  if (!workspace || workspace_bytes < need) return MXA_ERR_WORKSPACE;
+  const int nbk = (K + 31) / 32, kpad = nbk * 32;
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  int8_t* ac = reinterpret_cast<int8_t*>(ws);
+  int16_t* as = reinterpret_cast<int16_t*>(ws + align_up(batch * M * kpad));
+  int8_t* bt = reinterpret_cast<int8_t*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2));
+  int16_t* bsc = reinterpret_cast<int16_t*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) +
+                                            align_up(batch * Nc * kpad));
+  RowsPrepArgs ra{};
+  ra.x = a; ra.s0 = a_batch_stride; ra.s1 = 0; ra.s2 = K; ra.H = 1; ra.R = M; ra.rows = batch * M;
+  ra.D = K; ra.nb = nbk; ra.dpad = kpad;
+  ra.vec4 = aligned16(a) && (a_batch_stride % 4 == 0) && (K % 4 == 0);
+  ra.op_kind = elem_mbits_a == 8 ? MXA_OP_MXINT8 : MXA_OP_MXINT4;
+  ra.flush = flush_subnormals; ra.bfloat = bfloat;
+  ra.codes = nullptr; ra.sT = nullptr; ra.op = ac; ra.sA = as;
+  int rc = launch_rows_prep(ra, stream);
+  if (rc) return rc;
+  ColsPrepArgs cb{};
+  cb.x = b; cb.s0 = b_batch_stride; cb.s1 = 0; cb.s2 = Nc; cb.H = 1; cb.mats = batch; cb.R = K; cb.C = Nc;
+  cb.nb = nbk; cb.rpad = kpad; cb.mbits = elem_mbits_b; cb.flush = flush_subnormals; cb.bfloat = bfloat;
+  cb.codes_t = bt; cb.scale = bsc;
+  rc = launch_cols_prep(cb, stream);
+  if (rc) return rc;
+  MatmulArgs ma{ac, as, bt, bsc, M, Nc, nbk, kpad, bfloat, c};
+  dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 15) / 16), (unsigned)batch);
+  hipLaunchKernelGGL(matmul_kernel, grid, dim3(256), 0, stream, ma);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_selftest_mfma(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream) {
+  if (!a || !b || !c) return MXA_ERR_ARG;
+  hipLaunchKernelGGL(selftest_mfma_kernel, dim3(1), dim3(64), 0, stream, a, b, c);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}

@@ -1,0 +1,152 @@
+// Device helpers shared by every MX kernel (gfx950 / CDNA4, wave64).
+//
+// Numerics follow the reference's *Python* path bit for bit (the workloads
+// run it with custom_cuda=False), not the reference's CUDA
+// kernels, which use exponent bits and therefore disagree:
+//   shared exponent   microxscaling/mx/mx_ops.py:49-99
+//   scale clamp       microxscaling/mx/mx_ops.py:276-300
+//   element rounding  microxscaling/mx/elemwise_ops.py:45-86, :92-180
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mxa_exp_lut.h"
+
+namespace mxa {
+
+// int sentinel for a NaN shared exponent (NaN/Inf in the block, or scale overflow)
+constexpr int kExpNaN = -1000000;
+// int16 storage of the same sentinel
+constexpr int16_t kExpNaN16 = INT16_MIN;
+
+enum Round : int { kRoundNearest = 0, kRoundFloor = 1, kRoundEven = 2 };  // formats.py:12-16
+
+static __constant__ int32_t c_th_norm[256] = MXA_TH_NORM_INIT;
+static __constant__ int32_t c_th_sub[23] = MXA_TH_SUB_INIT;
+
+// floor(torch.log2(m + 2^-126 * (m == 0))) for m = |x| given as float bits with
+// the sign cleared (mx_ops.py:83-87).  Exact for every float32.
+__device__ __forceinline__ int floor_log2_abs_bits(uint32_t ub) {
+  if (ub >= 0x7F800000u) return kExpNaN;  // Inf / NaN -> NaN exponent (log2(inf)=inf > emax)
+  if (ub == 0u) return -126;
+  const uint32_t E = ub >> 23, M = ub & 0x7FFFFFu;
+  if (E) return (int)E - 127 + (M >= (uint32_t)c_th_norm[E] ? 1 : 0);
+  const int j = 31 - __clz((int)M);
+  return -149 + j + (M >= (uint32_t)c_th_sub[j] ? 1 : 0);
+}
+
+// Same rule without the zero trick: floor(log2(m)) of a strictly positive finite m.
+__device__ __forceinline__ int floor_log2_pos(float m) { return floor_log2_abs_bits(__float_as_uint(m)); }
+
+// exact 2^e as float for e in [-149, 127]
+__device__ __forceinline__ float pow2f(int e) {
+  return e >= -126 ? __uint_as_float((uint32_t)(e + 127) << 23) : __uint_as_float(1u << (e + 149));
+}
+// exact 2^e as double for e in [-1022, 1023]
+__device__ __forceinline__ double pow2d(int e) {
+  return __longlong_as_double((long long)(e + 1023) << 52);
+}
+
+__device__ __forceinline__ int16_t exp_to16(int e) { return e == kExpNaN ? kExpNaN16 : (int16_t)e; }
+__device__ __forceinline__ int exp_from16(int16_t e) { return e == kExpNaN16 ? kExpNaN : (int)e; }
+
+// Shared exponent of a block from the bits of its max |x|, after the optional
+// subnormal flush test and the scale clamp (mx_ops.py:276-291).  Returns the
+// raw exponent through *e_raw for the flush decision.
+__device__ __forceinline__ int scale_exponent(uint32_t maxbits, int scale_emax, int* e_raw) {
+  const int e = floor_log2_abs_bits(maxbits);
+  *e_raw = e;
+  if (e == kExpNaN || e > scale_emax) return kExpNaN;  // shared_exp > scale_emax -> NaN
+  return e < -scale_emax ? -scale_emax : e;
+}
+
+// Element rounding of x / 2^es * 2^(mbits-2) (elemwise_ops.py:45-65, :150-164);
+// returns the integer code as float, clamped to +-(2^(mbits-1)-1).
+// es is finite and in [-127, 127], so 2^-es is an exact float and x * 2^-es is
+// the correctly rounded x / 2^es.  Compiled with -ffp-contract=off.
+__device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd) {
+  float y = x * pow2f(-es);
+  y = y * (float)(1 << (mbits - 2));
+  const float a = fabsf(y);
+  float r;
+  if (rnd == kRoundFloor) {
+    r = floorf(a);
+  } else {
+    r = floorf(a + 0.5f);
+    if (rnd == kRoundEven) {
+      const float d = a - 0.5f;  // ((|A| - 0.5) % 2 == 0) -> step back to even
+      if (floorf(d * 0.5f) * 2.0f == d) r -= 1.0f;
+    }
+  }
+  const float lim = (float)((1 << (mbits - 1)) - 1);
+  r = r > lim ? lim : r;
+  return y < 0.0f ? -r : r;
+}
+
+// bfloatX element quantization, exp_bits = 8, mbits = bfloat-7 (elemwise_ops.py:201-216
+// -> _quantize_elemwise_core :92-180 with saturate_normals=False).  bfloat in {0,32} = identity.
+__device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int allow_denorm) {
+  if (bfloat == 0 || bfloat == 32) return x;
+  const uint32_t ub = __float_as_uint(x) & 0x7FFFFFFFu;
+  if (ub >= 0x7F800000u) return x;  // +-Inf restored, NaN stays NaN
+  const int bits = bfloat - 7;
+  float xin = x;
+  if (!allow_denorm && ub < 0x00800000u) xin = 0.0f * x;  // |A| < min_norm -> 0 (sign kept)
+  int pe = ub == 0u ? 0 : floor_log2_abs_bits(ub);  // log2(|A| + (A==0))
+  pe = pe < -126 ? -126 : pe;
+  float y = xin * pow2f(-pe);
+  y = y * (float)(1 << (bits - 2));
+  const float a = fabsf(y);
+  float r;
+  if (rnd == kRoundFloor) {
+    r = floorf(a);
+  } else {
+    r = floorf(a + 0.5f);
+    if (rnd == kRoundEven) {
+      const float d = a - 0.5f;
+      if (floorf(d * 0.5f) * 2.0f == d) r -= 1.0f;
+    }
+  }
+  float o = (y < 0.0f ? -r : r) * (1.0f / (float)(1 << (bits - 2)));
+  o = o * pow2f(pe > 127 ? 127 : pe);
+  const float max_norm = 1.7014118346046923e38f * ((float)((1 << (bits - 1)) - 1) / (float)(1 << (bits - 2)));
+  if (fabsf(o) > max_norm) o = o < 0.0f ? -INFINITY : INFINITY;
+  return o;
+}
+
+// ---- wave64 helpers -------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// LDS ordering between the lanes of one wave (no workgroup barrier needed).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace mxa

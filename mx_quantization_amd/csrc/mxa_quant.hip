@@ -1,0 +1,426 @@
+// MX quantization kernels for gfx950 (wave64).
+//
+//   mxa_quantize_mx        generic quantize_mx_op replacement (mx_ops.py:180-341)
+//   mxa_shared_exponents   _shared_exponents replacement      (mx_ops.py:49-99)
+//   mxa_quantize_bfloat    quantize_elemwise_op (bfloat)      (elemwise_ops.py:201-277)
+//   mxa_approx_values      exponent_approximation operands    (funcs/exponent_based_prediction.py)
+//   rows_prep / cols_prep  the attention path's operand builders (int8 codes + block
+//                          exponents + approximator operands), used by mxa_attn.hip
+//
+// All of it is HBM-bound byte work: coalesced fp32 loads, 32-element blocks
+// reduced with lane shuffles, int8 codes + int16 block exponents written out.
+#include "mxa_kernels.hpp"
+
+namespace mxa {
+
+// ---------------------------------------------------------------------------
+// generic MX quantize of a (outer, L, inner) tensor, one thread per block
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void quantize_mx_kernel(QuantArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nblocks = a.outer * a.nb * a.inner;
+  if (t >= nblocks) return;
+  const int64_t i = t % a.inner;
+  const int64_t ob = t / a.inner;
+  const int64_t blk = ob % a.nb;
+  const int64_t o = ob / a.nb;
+  const int64_t l0 = blk * a.bs;
+  const int64_t l1 = (l0 + a.bs < a.L) ? l0 + a.bs : a.L;
+  const float* xp = a.x + (o * a.L) * a.inner + i;
+  uint32_t mb = 0;
+  for (int64_t l = l0; l < l1; ++l) {
+    const uint32_t ub = __float_as_uint(round_bfloat(xp[l * a.inner], a.bfloat, kRoundNearest, 1)) & 0x7FFFFFFFu;
+    mb = ub > mb ? ub : mb;
+  }
+  int e_raw;
+  const int es = scale_exponent(mb, a.scale_emax, &e_raw);
+  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  const int shift = a.mbits - 2;
+  for (int64_t l = l0; l < l1; ++l) {
+    float xv = round_bfloat(xp[l * a.inner], a.bfloat, kRoundNearest, 1);
+    if (flush) xv = xv * 0.0f;
+    float yv, cv = 0.0f;
+    if (es == kExpNaN) {
+      yv = __uint_as_float(0x7FC00000u);
+    } else {
+      cv = round_code(xv, es, a.mbits, a.rnd);
+      yv = (cv * pow2f(-shift)) * pow2f(es);
+    }
+    const int64_t off = (o * a.L + l) * a.inner + i;
+    a.y[off] = yv;
+    if (a.codes) a.codes[off] = (int8_t)cv;
+  }
+  if (a.exps) a.exps[(o * a.nb + blk) * a.inner + i] = exp_to16(es);
+}
+
+// ---------------------------------------------------------------------------
+// shared exponents (method "max" per block, or "none" per element)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sexp_value(uint32_t ub, int ebits) {
+  int e = floor_log2_abs_bits(ub & 0x7FFFFFFFu);
+  float v;
+  if (e == kExpNaN) {
+    // log2(inf) = inf -> floor = inf; NaN stays NaN
+    v = ((ub & 0x7FFFFFFFu) == 0x7F800000u) ? INFINITY : __uint_as_float(0x7FC00000u);
+  } else {
+    v = (float)e;
+  }
+  if (ebits > 0) {
+    const float emax = (float)((1 << (ebits - 1)) - 1);
+    if (v > emax) v = __uint_as_float(0x7FC00000u);
+    else if (v < -emax) v = -emax;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void shared_exp_kernel(SexpArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.method == 1) {  // none: elementwise
+    const int64_t n = a.outer * a.L * a.inner;
+    if (t >= n) return;
+    a.out[t] = sexp_value(__float_as_uint(a.x[t]) & 0x7FFFFFFFu, a.ebits);
+    return;
+  }
+  const int64_t nblocks = a.outer * a.nb * a.inner;
+  if (t >= nblocks) return;
+  const int64_t i = t % a.inner;
+  const int64_t ob = t / a.inner;
+  const int64_t blk = ob % a.nb;
+  const int64_t o = ob / a.nb;
+  const int64_t l0 = blk * a.bs;
+  const int64_t l1 = (l0 + a.bs < a.L) ? l0 + a.bs : a.L;
+  uint32_t mb = 0;
+  for (int64_t l = l0; l < l1; ++l) {
+    const uint32_t ub = __float_as_uint(a.x[(o * a.L + l) * a.inner + i]) & 0x7FFFFFFFu;
+    mb = ub > mb ? ub : mb;  // NaN bits compare above Inf: max propagates NaN like torch.max
+  }
+  a.out[t] = sexp_value(mb, a.ebits);
+}
+
+// ---------------------------------------------------------------------------
+// elementwise bfloat quantization (vectorized, grid-stride)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bfloat_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                                     int bfloat, int rnd, int allow_denorm) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride)
+    y[t] = round_bfloat(x[t], bfloat, rnd, allow_denorm);
+}
+
+// ---------------------------------------------------------------------------
+// attention operand builder for rows quantized along the last axis (Q, K).
+// 8 lanes per 32-element block, 4 floats (16 B) per lane.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int exion_m(int raw) {
+  // two_step_leading_ones on an integer code (funcs/exponent_based_prediction.py:110-127):
+  //   l1 = floor(log2|raw|), t = max(raw - 2^l1, 0) (signed!), l2 = floor(log2 t),
+  //   approx = sign(raw) * e * (2^l1 + 2^l2) / 64   (2^-126 terms vanish in fp32)
+  if (raw == 0) return 0;
+  if (raw < 0) return -(1 << (31 - __clz(-raw)));
+  const int p1 = 1 << (31 - __clz(raw));
+  const int t = raw - p1;
+  return p1 + (t > 0 ? (1 << (31 - __clz(t))) : 0);
+}
+
+__global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sub = threadIdx.x & 7;
+  const int64_t g = gt >> 3;
+  const int64_t ngroups = a.rows * a.nb;
+  const bool valid = g < ngroups;
+  const int64_t row = valid ? g / a.nb : 0;
+  const int blk = valid ? (int)(g % a.nb) : 0;
+  const int64_t r = row % a.R;
+  const int64_t bh = row / a.R;
+  const int64_t h = bh % a.H;
+  const int64_t b = bh / a.H;
+  const float* xr = a.x + b * a.s0 + h * a.s1 + r * a.s2;
+  const int c0 = blk * 32 + sub * 4;
+  float xv[4];
+  if (valid && a.vec4 && c0 + 4 <= a.D) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + c0);
+    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = (valid && c0 + j < a.D) ? xr[c0 + j] : 0.0f;
+  }
+  uint32_t mb = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    xv[j] = round_bfloat(xv[j], a.bfloat, kRoundNearest, 1);
+    const uint32_t ub = __float_as_uint(xv[j]) & 0x7FFFFFFFu;
+    mb = ub > mb ? ub : mb;
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)mb, o, 8);
+    mb = w > mb ? w : mb;
+  }
+  int e_raw;
+  const int es = scale_exponent(mb, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  if (a.flush && !(e_raw != kExpNaN && e_raw > -127)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = xv[j] * 0.0f;
+  }
+  int code[4];
+  int maxc = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    code[j] = nanblk ? 0 : (int)round_code(xv[j], es, 8, kRoundNearest);
+    const int ac = code[j] < 0 ? -code[j] : code[j];
+    maxc = ac > maxc ? ac : maxc;
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const int w = __shfl_xor(maxc, o, 8);
+    maxc = w > maxc ? w : maxc;
+  }
+  // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
+  // floor(log2(max |MX|)), unclamped; MX max = maxc * 2^(es-6) exactly.
+  int eA;
+  if (nanblk) eA = kExpNaN;
+  else if (maxc == 0) eA = -126;
+  else eA = floor_log2_pos((float)maxc * pow2f(es - 6));
+  int op[4];
+  int sA;
+  switch (a.op_kind) {
+    case MXA_OP_SIGN:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = (c0 + j < a.D) ? (code[j] < 0 ? -1 : 1) : 0;
+      sA = eA;
+      break;
+    case MXA_OP_MXINT4:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest);
+      sA = nanblk ? kExpNaN : es - 2;
+      break;
+    case MXA_OP_EXION: {
+      const int sh = nanblk ? 0 : es - eA;  // MX / 2^eA * 64 = code * 2^(es-eA), an integer < 128
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : exion_m(code[j] << sh);
+      sA = eA;
+      break;
+    }
+    default:  // MXA_OP_MXINT8
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = code[j];
+      sA = nanblk ? kExpNaN : es - 6;
+      break;
+  }
+  if (valid) {
+    const int64_t base = row * a.dpad + c0;
+    const uint32_t pc = (uint32_t)(code[0] & 0xFF) | ((uint32_t)(code[1] & 0xFF) << 8) |
+                        ((uint32_t)(code[2] & 0xFF) << 16) | ((uint32_t)(code[3] & 0xFF) << 24);
+    const uint32_t po = (uint32_t)(op[0] & 0xFF) | ((uint32_t)(op[1] & 0xFF) << 8) |
+                        ((uint32_t)(op[2] & 0xFF) << 16) | ((uint32_t)(op[3] & 0xFF) << 24);
+    if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
+    if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
+    if (sub == 0) {
+      if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
+      if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// operand builder for matrices quantized along the row axis (V, and in2 of
+// mx.matmul): blocks of 32 rows per column; output transposed [col][row] codes.
+// One thread per (matrix, block, column): coalesced along columns.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = a.mats * a.nb * a.C;
+  if (t >= total) return;
+  const int c = (int)(t % a.C);
+  const int64_t mb_ = t / a.C;
+  const int blk = (int)(mb_ % a.nb);
+  const int64_t m = mb_ / a.nb;
+  const int64_t h = m % a.H;
+  const int64_t b = m / a.H;
+  const float* xc = a.x + b * a.s0 + h * a.s1 + c;
+  const int r0 = blk * 32;
+  float xv[32];
+  uint32_t mx = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int rr = r0 + j;
+    float v = rr < a.R ? xc[(int64_t)rr * a.s2] : 0.0f;
+    v = round_bfloat(v, a.bfloat, kRoundNearest, 1);
+    xv[j] = v;
+    const uint32_t ub = __float_as_uint(v) & 0x7FFFFFFFu;
+    mx = ub > mx ? ub : mx;
+  }
+  int e_raw;
+  const int es = scale_exponent(mx, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  uint32_t w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = xv[q * 4 + j];
+      if (flush) v = v * 0.0f;
+      const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest);
+      acc |= (uint32_t)(cd & 0xFF) << (8 * j);
+    }
+    w[q] = acc;
+  }
+  int8_t* dst = a.codes_t + (m * a.C + c) * a.rpad + r0;
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  a.scale[(m * a.nb + blk) * a.C + c] = exp_to16(nanblk ? kExpNaN : es - (a.mbits - 2));
+}
+
+// ---------------------------------------------------------------------------
+// approximator operand VALUES (what exponent_approximation's methods return)
+// one thread per (row, 32-block); exact fp32 op order of the reference.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = (a.d + 31) / 32;
+  if (t >= a.rows * nb) return;
+  const int64_t row = t / nb;
+  const int blk = (int)(t % nb);
+  const float* xr = a.x + row * a.ld_x;
+  float* yr = a.out + row * a.ld_out;
+  const int c0 = blk * 32, c1 = (c0 + 32 < a.d) ? c0 + 32 : a.d;
+  uint32_t mb = 0;
+  for (int c = c0; c < c1; ++c) {
+    const uint32_t ub = __float_as_uint(round_bfloat(xr[c], a.bfloat, kRoundNearest, 1)) & 0x7FFFFFFFu;
+    mb = ub > mb ? ub : mb;
+  }
+  int e_raw;
+  const int es = scale_exponent(mb, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  const float qnan = __uint_as_float(0x7FC00000u);
+  int maxc = 0;
+  for (int c = c0; c < c1; ++c) {
+    float xv = round_bfloat(xr[c], a.bfloat, kRoundNearest, 1);
+    if (flush) xv = xv * 0.0f;
+    const int cd = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+    maxc = (cd < 0 ? -cd : cd) > maxc ? (cd < 0 ? -cd : cd) : maxc;
+  }
+  const int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : floor_log2_pos((float)maxc * pow2f(es - 6)));
+  for (int c = c0; c < c1; ++c) {
+    float xv = round_bfloat(xr[c], a.bfloat, kRoundNearest, 1);
+    if (flush) xv = xv * 0.0f;
+    float out;
+    if (nanblk) {
+      out = qnan;
+    } else if (a.op_kind == MXA_OP_MXINT4) {
+      out = (round_code(xv, es, 4, kRoundNearest) * 0.25f) * pow2f(es);
+    } else {
+      const int cd = (int)round_code(xv, es, 8, kRoundNearest);
+      const float mxv = ((float)cd * pow2f(-6)) * pow2f(es);  // MX int8 value
+      switch (a.op_kind) {
+        case MXA_OP_SIGN:  // (mx < 0 ? -1 : +1) * 2^eA
+          out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(eA);
+          break;
+        case MXA_OP_EXION: {  // sign(mx) * eA * (2^l1 + 2^l2) / 64
+          const int m = exion_m(cd << (es - eA));
+          const float sg = cd > 0 ? 1.0f : (cd < 0 ? -1.0f : 0.0f);
+          out = ((sg * (float)eA) * (float)(m < 0 ? -m : m)) / 64.0f;
+          break;
+        }
+        case MXA_OP_TRUE_EX: {  // (mx < 0 ? -1 : +1) * 2^(floor(log2|mx|)), zeros -> 2^0
+          const float am = fabsf(mxv);
+          const int te = am > 0.0f ? floor_log2_pos(am) : 0;
+          out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(te);
+          break;
+        }
+        default:
+          out = mxv;
+      }
+    }
+    yr[c] = out;
+  }
+}
+
+}  // namespace mxa
+
+using namespace mxa;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int mxa_quantize_mx(const float* x, float* y, int8_t* codes, int16_t* exps, int64_t outer,
+                               int64_t axis_len, int64_t inner, int32_t block_size, int32_t elem_mbits,
+                               int32_t scale_bits, int32_t round_mode, int32_t flush_subnormals, int32_t bfloat,
+                               hipStream_t stream) {
+  if (!x || !y || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0) return MXA_ERR_ARG;
+  if (elem_mbits != 8 && elem_mbits != 4 && elem_mbits != 2) return MXA_ERR_UNSUPPORTED;
+  if (scale_bits < 2 || scale_bits > 8 || round_mode < 0 || round_mode > 2) return MXA_ERR_ARG;
+  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
+  if (outer == 0 || axis_len == 0 || inner == 0) return MXA_OK;
+  QuantArgs a{};
+  a.x = x; a.y = y; a.codes = codes; a.exps = exps;
+  a.outer = outer; a.L = axis_len; a.inner = inner;
+  a.bs = block_size == 0 ? axis_len : block_size;
+  a.nb = (axis_len + a.bs - 1) / a.bs;
+  a.mbits = elem_mbits; a.scale_emax = (1 << (scale_bits - 1)) - 1; a.rnd = round_mode;
+  a.flush = flush_subnormals; a.bfloat = bfloat;
+  const int64_t nblocks = outer * a.nb * inner;
+  hipLaunchKernelGGL(quantize_mx_kernel, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_shared_exponents(const float* x, float* out, int64_t outer, int64_t axis_len, int64_t inner,
+                                    int32_t block_size, int32_t method, int32_t ebits, hipStream_t stream) {
+  if (!x || !out || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0) return MXA_ERR_ARG;
+  if (method != 0 && method != 1) return MXA_ERR_ARG;
+  if (outer == 0 || axis_len == 0 || inner == 0) return MXA_OK;
+  SexpArgs a{};
+  a.x = x; a.out = out; a.outer = outer; a.L = axis_len; a.inner = inner;
+  a.bs = block_size == 0 ? axis_len : block_size;
+  a.nb = (axis_len + a.bs - 1) / a.bs;
+  a.method = method; a.ebits = ebits;
+  const int64_t n = method == 1 ? outer * axis_len * inner : outer * a.nb * inner;
+  hipLaunchKernelGGL(shared_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_quantize_bfloat(const float* x, float* y, int64_t n, int32_t bfloat, int32_t round_mode,
+                                   int32_t allow_denorm, hipStream_t stream) {
+  if (!x || !y || n < 0) return MXA_ERR_ARG;
+  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
+  if (round_mode < 0 || round_mode > 2) return MXA_ERR_ARG;
+  if (n == 0) return MXA_OK;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipLaunchKernelGGL(bfloat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, n, bfloat, round_mode,
+                     allow_denorm);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64_t ld_x, int64_t ld_out,
+                                 int32_t op_kind, int32_t flush_subnormals, int32_t bfloat, hipStream_t stream) {
+  if (!x || !out || rows < 0 || d <= 0 || ld_x < d || ld_out < d) return MXA_ERR_ARG;
+  if (op_kind < MXA_OP_SIGN || op_kind > MXA_OP_TRUE_EX) return MXA_ERR_ARG;
+  if (rows == 0) return MXA_OK;
+  ApproxArgs a{};
+  a.x = x; a.out = out; a.rows = rows; a.d = d; a.ld_x = ld_x; a.ld_out = ld_out;
+  a.op_kind = op_kind; a.flush = flush_subnormals; a.bfloat = bfloat;
+  const int64_t n = rows * ((d + 31) / 32);
+  hipLaunchKernelGGL(approx_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+namespace mxa {
+int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream) {
+  const int64_t threads = a.rows * a.nb * 8;
+  if (threads == 0) return MXA_OK;
+  hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream) {
+  const int64_t threads = a.mats * a.nb * a.C;
+  if (threads == 0) return MXA_OK;
+  hipLaunchKernelGGL(cols_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+}  // namespace mxa

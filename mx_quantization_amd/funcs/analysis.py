@@ -1,0 +1,101 @@
+"""Approximation-quality hooks -- funcs/analysis.py surface (the `--anal` runs).
+File writers and index statistics; torch ops on whatever device idx lives on."""
+from __future__ import annotations
+
+import ast
+import os
+import re
+from pathlib import Path
+
+import torch
+
+
+def create_file(output_file):
+    d = os.path.dirname(output_file)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    open(output_file, "w").close()
+
+
+def save_idx_file(idx, output_file, block_idx=None):
+    """Per head / token index lists of batch element 1 (analysis.py:22-29)."""
+    _, H, N, _ = idx.shape
+    with open(output_file, "a") as f:
+        f.write(f"Cross-attention Block {block_idx}\n")
+        for h in range(H):
+            f.write(f" Head {h}:\n")
+            for n in range(N):
+                f.write(f"  Token {n:3d}: {idx[1, h, n, :].tolist()}\n")
+
+
+def save_diff_score_file(diff_score, output_file, block_idx=None):
+    with open(output_file, "a") as f:
+        f.write(f"{diff_score}\n")
+
+
+def init_analysis_files(attn_type, anal_dir, k, approx_flag, pred_mode, total_timestep):
+    """File-name table per timestep (analysis.py:35-54)."""
+    d = f"{anal_dir}/{attn_type}"
+    d = f"{d}/{pred_mode}" if approx_flag else f"{d}/true"
+    table = {}
+    for t in range(total_timestep):
+        table[t] = {
+            "idx": f"{d}/top{k}_idx_t{t}.txt",
+            "vals": f"{d}/top{k}_vals_t{t}.txt",
+            "diff_idx": f"{d}/top{k}_diff_idx_t{t}.txt",
+        }
+        create_file(table[t]["diff_idx"])
+    return table
+
+
+def total_chosen_k(pred_idx):
+    """Mean over (batch, head) of |unique chosen keys| / rows (analysis.py:56-110)."""
+    B, H = pred_idx.shape[0], pred_idx.shape[1]
+    rows = pred_idx.shape[-2]
+    total = 0.0
+    for b in range(B):
+        for h in range(H):
+            total += torch.unique(pred_idx[b, h].flatten()).numel() / rows
+    return total / (B * H)
+
+
+def diff_idx_analysis(true_idx: torch.Tensor, pred_idx: torch.Tensor):
+    """Share of the true top-k score mass the predicted top-k keeps, over the first
+    100 batch entries (analysis.py:136-157)."""
+    present = torch.isin(true_idx, pred_idx)
+    kept = torch.where(present, true_idx, torch.zeros_like(true_idx))
+    ratio = kept.sum(dim=-1, keepdim=True) / true_idx.sum(dim=-1, keepdim=True)
+    return ratio[0:100, :, :, 0].sum().item() / (100 * ratio.shape[1] * ratio.shape[2])
+
+
+def parse_tokens(path, token_re):
+    """{block: {head: {token: list}}} from save_idx_file output."""
+    tokens = {}
+    block_idx = head_idx = 0
+    with Path(path).open() as f:
+        for line in f:
+            m = token_re.search(line)
+            if not m:
+                continue
+            tid = int(m.group(2))
+            tokens.setdefault(block_idx, {}).setdefault(head_idx, {})[tid] = ast.literal_eval(m.group(3))
+            if tid == 255 and head_idx == 15:
+                head_idx, block_idx = 0, block_idx + 1
+            elif tid == 255:
+                head_idx += 1
+    return tokens
+
+
+def mismatch_analysis(true_top20_file, pred_top60_file):
+    """Fraction of true top-k indices missing from the predicted lists, per file pair."""
+    token_re = re.compile(r"(Token\s+)(\d+):\s*(\[.*\])")
+    true_t = parse_tokens(true_top20_file, token_re)
+    pred_t = parse_tokens(pred_top60_file, token_re)
+    miss = tot = 0
+    for b, heads in true_t.items():
+        for h, toks in heads.items():
+            for t, lst in toks.items():
+                p = set(pred_t.get(b, {}).get(h, {}).get(t, []))
+                miss += sum(1 for x in lst if x not in p)
+                tot += len(lst)
+    return miss / tot if tot else 0.0

@@ -1,0 +1,104 @@
+"""Approximator API -- drop-in for funcs/exponent_based_prediction.py.
+
+`exponent_approximation(Q, K, mx_specs)` keeps the reference's constructor and
+method names; every method returns (approx_Q, approx_K) with the shape of Q and
+K, computed by libmxa.so (mxa_approx_values) on the device.
+
+Differences from the reference, all deliberate:
+  * exponent_based_sign() implements the INTENDED exp-sign semantics.  In
+    funcs/ it raises UnboundLocalError (the two lines defining
+    expanded_exponents_Q/K are commented out, :80-81 vs :85-86);
+    the working copy microxscaling/examples/deit/exponent_based_prediction.py:135-161
+    and partial_K/partial_Q (:284-293, :309-313) define the values (F2).
+  * exponent_based_sign_leading_ones() ("true_ex") comes from the examples copy
+    (:163-178), which the PixArt modules call.
+  * Methods do not `del` instance attributes (:92, :270); callers build a fresh
+    object per forward, so nothing observes the difference.
+Block size 32 (the workloads' mx_specs) is required.
+"""
+from __future__ import annotations
+
+from .. import ops
+from ..mx.elemwise_ops import quantize_elemwise_op
+from ..mx.mx_ops import _reshape_to_blocks, _shared_exponents, quantize_mx_op
+
+
+class exponent_approximation:
+    def __init__(self, Q, K, mx_specs):
+        self.mx_specs = mx_specs
+        if mx_specs["block_size"] != 32:
+            raise NotImplementedError("approximators are built for 32-element MX blocks")
+        if mx_specs["round_mx_output"] != "nearest":
+            raise NotImplementedError("approximators are built for round_mx_output='nearest'")
+        self.Q = quantize_elemwise_op(Q, mx_specs, round=mx_specs["round_output"]).float()
+        self.K = quantize_elemwise_op(K, mx_specs, round=mx_specs["round_output"]).float()
+        self.shared_exponent_method = mx_specs.get("shared_exp_method", "max")
+        self._flush = bool(mx_specs["mx_flush_fp32_subnorms"])
+        # MXINT8 copies (funcs/exponent_based_prediction.py:18-31)
+        self.MX_Q = quantize_mx_op(self.Q, mx_specs, elem_format=mx_specs["a_elem_format"], axes=[-1],
+                                   round=mx_specs["round_mx_output"])
+        self.MX_K = quantize_mx_op(self.K, mx_specs, elem_format=mx_specs["a_elem_format"], axes=[-1],
+                                   round=mx_specs["round_mx_output"])
+
+    # -- reference attributes, built on first use (:33-38) ----------------------
+    def _blocks(self):
+        if not hasattr(self, "reshaped_MX_Q"):
+            bs = self.mx_specs["block_size"]
+            (self.reshaped_MX_Q, self.axes_Q, self.orig_shape_Q,
+             self.padded_shape_Q) = _reshape_to_blocks(self.MX_Q, [-1], bs)
+            (self.reshaped_MX_K, self.axes_K, self.orig_shape_K,
+             self.padded_shape_K) = _reshape_to_blocks(self.MX_K, [-1], bs)
+
+    @property
+    def shared_exponent_Q(self):
+        self._blocks()
+        return _shared_exponents(self.reshaped_MX_Q, method=self.shared_exponent_method, axes=[-1], ebits=0)
+
+    @property
+    def shared_exponent_K(self):
+        self._blocks()
+        return _shared_exponents(self.reshaped_MX_K, method=self.shared_exponent_method, axes=[-1], ebits=0)
+
+    @property
+    def true_exponent_Q(self):
+        self._blocks()
+        return _shared_exponents(self.reshaped_MX_Q, method="none", axes=[-1], ebits=0)
+
+    @property
+    def true_exponent_K(self):
+        self._blocks()
+        return _shared_exponents(self.reshaped_MX_K, method="none", axes=[-1], ebits=0)
+
+    # -- approximators -----------------------------------------------------------
+    def _vals(self, X, kind):
+        return ops.approx_values(X, kind, flush=self._flush)
+
+    def exponent_based_sign(self):
+        """Proposed exp-sign: (mx < 0 ? -1 : +1) * 2^(shared exponent of the MX block)."""
+        return self._vals(self.Q, "sign"), self._vals(self.K, "sign")
+
+    def two_step_leading_ones(self):
+        """EXION (:96-177), including the e * (2^l1 + 2^l2) / 64 quirk of :126-127."""
+        return self._vals(self.Q, "exion"), self._vals(self.K, "exion")
+
+    def MXINT4(self):
+        """Sanger: MXINT4 Q and K (:179-272)."""
+        return self._vals(self.Q, "mxint4"), self._vals(self.K, "mxint4")
+
+    def partial_K(self):
+        """Q exp-sign, K MXINT8 (:274-300)."""
+        return self._vals(self.Q, "sign"), self.MX_K
+
+    def partial_Q(self):
+        """Q MXINT8, K exp-sign (:302-318)."""
+        return self.MX_Q, self._vals(self.K, "sign")
+
+    def exponent_based_sign_leading_ones(self):
+        """true_ex: (mx < 0 ? -1 : +1) * 2^floor(log2|mx|), zeros -> +1
+        (examples/deit/exponent_based_prediction.py:163-178)."""
+        return self._vals(self.Q, "true_ex"), self._vals(self.K, "true_ex")
+
+    def exponent_based_threshold_exponent(self):
+        # funcs/exponent_based_prediction.py:320-340 calls get_true_exponents, which the
+        # class does not define: the reference raises AttributeError here too.
+        raise AttributeError("'exponent_approximation' object has no attribute 'get_true_exponents'")

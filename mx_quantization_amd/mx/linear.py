@@ -1,0 +1,69 @@
+"""MX Linear -- drop-in for microxscaling/mx/linear.py (forward / inference).
+
+out = MX(x, along in_features) @ MX(W, along in_features)^T (+ bias), on the
+device through mxa_matmul.  This is the qkv / proj projection around the
+attention core (a SURVEY §8f "next" row): present so the patched modules'
+`from mx import Linear` keeps working; its fusion into the attention kernels is
+future work."""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .elemwise_ops import quantize_elemwise_op
+from .matmul import _check_specs, _mbits
+from .specs import apply_mx_specs, mx_assert_test
+
+
+def linear(input, weight, bias=None, mx_specs=None, prequantized_weights=False, name=None):
+    """LinearFunction.forward (linear.py:20-103)."""
+    if mx_specs is None:
+        return torch.nn.functional.linear(input, weight, bias)
+    s = apply_mx_specs(mx_specs)
+    _check_specs(s)
+    bf_in = quantize_elemwise_op(input, mx_specs=s, round=s["round_output"]).float()
+    bf_w = weight.float() if prequantized_weights else quantize_elemwise_op(weight, mx_specs=s,
+                                                                             round=s["round_weight"]).float()
+    x2 = bf_in.reshape(1, -1, bf_in.shape[-1])
+    out = ops.mx_matmul(x2, bf_w.t().unsqueeze(0), _mbits(s["a_elem_format"]), _mbits(s["w_elem_format"]),
+                        flush=s["mx_flush_fp32_subnorms"])
+    out = out.reshape(bf_in.shape[:-1] + (weight.shape[0],))
+    out = quantize_elemwise_op(out, mx_specs=s, round=s["round_output"])
+    if bias is not None:
+        bb = bias.float() if prequantized_weights else quantize_elemwise_op(bias, mx_specs=s, round=s["round_weight"])
+        out = quantize_elemwise_op(out + bb, mx_specs=s, round=s["round_output"])
+    return out
+
+
+class Linear(torch.nn.Linear):
+    """linear.py:227-320 (inference)."""
+
+    def __init__(self, in_features, out_features, bias=True, mx_specs=None, name=None):
+        mx_assert_test(mx_specs)
+        self.mx_none = mx_specs is None
+        self.name = name
+        self.prequantized_weights = False
+        self.mx_specs = apply_mx_specs(mx_specs)
+        super().__init__(in_features, out_features, bias)
+
+    def apply_mx_specs(self, mx_specs):
+        mx_assert_test(mx_specs)
+        self.mx_none = mx_specs is None
+        self.mx_specs = apply_mx_specs(mx_specs)
+
+    def append_name(self, postfix):
+        self.name += postfix
+
+    def get_quantized_weight(self):
+        """The MX-quantized weight (linear.py:253-274)."""
+        if self.mx_none:
+            return self.weight
+        from .mx_ops import quantize_mx_op
+        bf_w = quantize_elemwise_op(self.weight, mx_specs=self.mx_specs, round=self.mx_specs["round_weight"])
+        return quantize_mx_op(bf_w, self.mx_specs, elem_format=self.mx_specs["w_elem_format"], axes=[-1],
+                              round=self.mx_specs["round_mx_output"])
+
+    def forward(self, inputs):
+        if self.mx_none:
+            return super().forward(inputs)
+        return linear(inputs, self.weight, self.bias, self.mx_specs, self.prequantized_weights, self.name)

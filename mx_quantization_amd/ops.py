@@ -1,0 +1,236 @@
+"""torch-facing wrappers over the C ABI.  torch only allocates and supplies the
+stream; every byte of arithmetic happens in libmxa.so on the MI355X."""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native as N
+from ._native import check, lib, require_device, stream_ptr
+
+_WS: dict = {}
+
+
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    key = (device, stream_ptr(device))
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    return t
+
+
+def _split(shape, axis):
+    axis = axis % len(shape) if len(shape) else 0
+    outer = 1
+    for s in shape[:axis]:
+        outer *= s
+    inner = 1
+    for s in shape[axis + 1:]:
+        inner *= s
+    return outer, (shape[axis] if len(shape) else 1), inner
+
+
+def quantize_mx(A: torch.Tensor, elem_mbits: int = 8, block_size: int = 32, axis: int = -1, scale_bits: int = 8,
+                round: str = "nearest", flush: bool = False, bfloat: int = 0, want_codes: bool = False):
+    """MX block quantization along one axis (mx_ops.py:180-306).  Returns the
+    dequantized tensor, plus (codes int8, block exponents int16) if want_codes."""
+    dev = require_device(A)
+    A = _f32(A, "A").contiguous()
+    y = torch.empty_like(A)
+    outer, L, inner = _split(tuple(A.shape), axis)
+    codes = exps = None
+    if want_codes:
+        bs = L if block_size == 0 else block_size
+        codes = torch.empty(A.shape, dtype=torch.int8, device=dev)
+        exps = torch.empty((outer, (L + bs - 1) // max(bs, 1), inner), dtype=torch.int16, device=dev)
+    if A.numel():
+        check(lib().mxa_quantize_mx(A.data_ptr(), y.data_ptr(), codes.data_ptr() if want_codes else None,
+                                    exps.data_ptr() if want_codes else None, outer, L, inner, block_size,
+                                    elem_mbits, scale_bits, N.ROUND_MODES[round], int(flush), int(bfloat),
+                                    stream_ptr(dev)), "mxa_quantize_mx")
+    return (y, codes, exps) if want_codes else y
+
+
+def shared_exponents(A: torch.Tensor, method: str = "max", axis: int = -1, block_size: int = 0,
+                     ebits: int = 0) -> torch.Tensor:
+    """_shared_exponents (mx_ops.py:49-99) for one axis; 'max' keeps the axis as
+    the block count (size 1 when block_size covers the axis)."""
+    dev = require_device(A)
+    A = _f32(A, "A").contiguous()
+    outer, L, inner = _split(tuple(A.shape), axis)
+    if method == "none":
+        out = torch.empty_like(A)
+        m = 1
+    elif method == "max":
+        bs = L if block_size == 0 else block_size
+        shape = list(A.shape)
+        shape[axis % A.dim()] = (L + bs - 1) // bs
+        out = torch.empty(shape, dtype=torch.float32, device=dev)
+        m = 0
+    else:
+        raise ValueError(f"Unrecognized shared exponent selection method {method}")
+    if A.numel():
+        check(lib().mxa_shared_exponents(A.data_ptr(), out.data_ptr(), outer, L, inner, block_size, m, ebits,
+                                         stream_ptr(dev)), "mxa_shared_exponents")
+    return out
+
+
+def quantize_bfloat(A: torch.Tensor, bfloat: int = 16, round: str = "nearest", allow_denorm: bool = True):
+    """bfloatX elementwise quantization (elemwise_ops.py:201-216)."""
+    dev = require_device(A)
+    A = _f32(A, "A").contiguous()
+    y = torch.empty_like(A)
+    if A.numel():
+        check(lib().mxa_quantize_bfloat(A.data_ptr(), y.data_ptr(), A.numel(), int(bfloat), N.ROUND_MODES[round],
+                                        int(allow_denorm), stream_ptr(dev)), "mxa_quantize_bfloat")
+    return y
+
+
+OP_KINDS = {"sign": N.MXA_OP_SIGN, "mxint8": N.MXA_OP_MXINT8, "mxint4": N.MXA_OP_MXINT4,
+            "exion": N.MXA_OP_EXION, "true_ex": N.MXA_OP_TRUE_EX}
+
+
+def approx_values(X: torch.Tensor, kind: str, flush: bool = False, bfloat: int = 0) -> torch.Tensor:
+    """Approximator operand values along the last axis (funcs/exponent_based_prediction.py)."""
+    dev = require_device(X)
+    X = _f32(X, "X").contiguous()
+    out = torch.empty_like(X)
+    d = X.shape[-1]
+    rows = X.numel() // d if d else 0
+    if rows:
+        check(lib().mxa_approx_values(X.data_ptr(), out.data_ptr(), rows, d, d, d, OP_KINDS[kind], int(flush),
+                                      int(bfloat), stream_ptr(dev)), "mxa_approx_values")
+    return out
+
+
+def topk(vals: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """torch.topk(vals, k, dim=-1, largest=True, sorted=True) with torch's CPU
+    index order (TopKImpl.h:45-86), computed on the device."""
+    dev = require_device(vals)
+    vals = _f32(vals, "vals").contiguous()
+    n = vals.shape[-1]
+    rows = vals.numel() // n if n else 0
+    idx = torch.empty(vals.shape[:-1] + (k,), dtype=torch.int64, device=dev)
+    out = torch.empty(vals.shape[:-1] + (k,), dtype=torch.float32, device=dev)
+    if rows and k:
+        check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(), stream_ptr(dev)),
+              "mxa_topk")
+    return out, idx
+
+
+def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbits_b: int = 8, flush: bool = False,
+              bfloat: int = 0) -> torch.Tensor:
+    """MX matmul forward (matmul.py:31-100): a (..., M, K) along K, b (..., K, Nc) along K."""
+    dev = require_device(a, b)
+    a = _f32(a, "in1")
+    b = _f32(b, "in2")
+    if a.dim() < 2 or b.dim() < 2:
+        raise ValueError("mx matmul needs >= 2-D operands")
+    batch_shape = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
+    M, K = a.shape[-2:]
+    K2, Nc = b.shape[-2:]
+    if K != K2:
+        raise ValueError(f"inner dimensions differ: {K} vs {K2}")
+    a = a.expand(batch_shape + (M, K)).contiguous()
+    b = b.expand(batch_shape + (K, Nc)).contiguous()
+    batch = 1
+    for s in batch_shape:
+        batch *= s
+    c = torch.empty(batch_shape + (M, Nc), dtype=torch.float32, device=dev)
+    if batch == 0 or M == 0 or Nc == 0:
+        return c
+    if K == 0:
+        return c.zero_()
+    nbytes = lib().mxa_matmul_workspace_bytes(batch, M, K, Nc)
+    ws = _workspace(dev, nbytes)
+    check(lib().mxa_matmul(a.data_ptr(), b.data_ptr(), c.data_ptr(), batch, M, K, Nc, M * K, K * Nc, elem_mbits_a,
+                           elem_mbits_b, int(flush), int(bfloat), ws.data_ptr(), ws.numel(), stream_ptr(dev)),
+          "mxa_matmul")
+    return c
+
+
+def _strides3(t: torch.Tensor, name: str):
+    if t.dim() != 4:
+        raise ValueError(f"{name} must be (B, H, rows, D)")
+    if t.stride(3) != 1:
+        raise ValueError(f"{name} must be contiguous in its last (head_dim) axis")
+    return (t.stride(0), t.stride(1), t.stride(2))
+
+
+def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, k_top: int = 20,
+                      pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
+                      bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
+                      return_scores: bool = False, out: Optional[torch.Tensor] = None):
+    """The fused hot path (include/mxa.h mxa_attention): q (B,H,N,D), k/v (B,H,T,D)
+    float32 (strided views of a packed qkv are fine).  Returns (out (B,H,N,D),
+    idx (B,H,N,k_top) int64 or None[, true, pred])."""
+    dev = require_device(q, k, v, bias)
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        _f32(t, nm)
+    B, H, Nq, D = q.shape
+    Bk, Hk, T, Dk = k.shape
+    if (Bk, Hk, Dk) != (B, H, D) or tuple(v.shape) != (B, H, T, D):
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if top_k and not (0 < k_top <= T):
+        raise ValueError(f"k={k_top} out of range for {T} keys")
+    if top_k and approx and pred_mode not in N.PRED_MODES:
+        raise ValueError(f"pred_mode {pred_mode!r} not supported by the fused op "
+                         f"(supported: {sorted(N.PRED_MODES)})")
+    p = N.AttnParams()
+    p.q, p.k, p.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+    p.q_strides[:] = _strides3(q, "q")
+    p.k_strides[:] = _strides3(k, "k")
+    p.v_strides[:] = _strides3(v, "v")
+    p.B, p.H, p.N, p.T, p.D = B, H, Nq, T, D
+    p.k_top = int(k_top) if top_k else 0
+    p.scale = float(torch.tensor(scale, dtype=torch.float32).item())  # torch: python scale -> fp32 operand
+    p.pred_mode = N.PRED_MODES.get(pred_mode, 0)
+    p.top_k, p.approx = int(bool(top_k)), int(bool(approx))
+    p.flush_subnormals, p.bfloat = int(bool(flush_subnormals)), int(bfloat)
+    if bias is not None:
+        _f32(bias, "bias")
+        bias4 = bias
+        while bias4.dim() < 4:
+            bias4 = bias4.unsqueeze(0)
+        bias4 = bias4.expand(B, H, Nq, T)
+        p.bias = bias4.data_ptr()
+        p.bias_strides[:] = tuple(bias4.stride())
+    if out is None:
+        out = torch.empty((B, H, Nq, D), dtype=torch.float32, device=dev)
+    p.out = out.data_ptr()
+    p.out_strides[:] = (out.stride(0), out.stride(1), out.stride(2))
+    if out.stride(3) != 1:
+        raise ValueError("out must be contiguous in its last axis")
+    idx = torch.empty((B, H, Nq, k_top), dtype=torch.int64, device=dev) if top_k else None
+    p.idx_out = idx.data_ptr() if idx is not None else None
+    true_s = pred_s = None
+    if return_scores:
+        true_s = torch.empty((B, H, Nq, T), dtype=torch.float32, device=dev)
+        pred_s = torch.full((B, H, Nq, T), float("nan"), dtype=torch.float32, device=dev)
+        p.true_out, p.pred_out = true_s.data_ptr(), pred_s.data_ptr()
+    nbytes = lib().mxa_attention_workspace_bytes(ctypes.byref(p))
+    if nbytes < 0:
+        raise ValueError("bad attention shape")
+    ws = _workspace(dev, nbytes)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    check(lib().mxa_attention(ctypes.byref(p), stream_ptr(dev)), "mxa_attention")
+    if return_scores:
+        return out, idx, true_s, pred_s
+    return out, idx
+
+
+def selftest_mfma(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    dev = require_device(a, b)
+    c = torch.empty((16, 16), dtype=torch.int32, device=dev)
+    check(lib().mxa_selftest_mfma(a.contiguous().data_ptr(), b.contiguous().data_ptr(), c.data_ptr(),
+                                  stream_ptr(dev)), "mxa_selftest_mfma")
+    return c

@@ -1,0 +1,98 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads and exports every
+symbol include/mxa.h declares, the Python surfaces import under the reference's
+names, and the product path refuses CPU tensors (no fallback)."""
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "mxa.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mxa_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mx_quantization_amd import _native as N
+    lib = N.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(N.EXPORTS), "ctypes signatures out of sync with include/mxa.h"
+    assert lib.mxa_abi_version() == 1
+
+
+def test_status_strings_and_arg_errors():
+    from mx_quantization_amd import _native as N
+    lib = N.lib()
+    assert lib.mxa_status_string(0) == b"ok"
+    # argument validation happens before any launch, so these run without a GPU
+    assert lib.mxa_quantize_mx(None, None, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, None) == -1
+    assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 5, 8, 0, 0, 0, None) == -2  # fp formats
+    assert lib.mxa_topk(1, 1, 600, 600, 3, 1, None, None) == -2  # n > 512
+    assert lib.mxa_topk(1, 1, 10, 10, 11, 1, None, None) == -1  # k > n
+    p = N.AttnParams()
+    assert lib.mxa_attention_workspace_bytes(p) == -1
+    assert lib.mxa_attention(p, None) == -1
+
+
+def test_workspace_formula():
+    import ctypes
+    from mx_quantization_amd import _native as N
+    p = N.AttnParams()
+    p.B, p.H, p.N, p.T, p.D = 256, 12, 197, 197, 64
+    nbytes = N.lib().mxa_attention_workspace_bytes(ctypes.byref(p))
+    # per head: Q,K codes + approx operands (4 x 197 x 64 B), P codes (197 x 224 B), V^T (64 x 224 B)
+    assert 3072 * (197 * (64 * 4 + 224) + 64 * 224) < nbytes < 3072 * 197 * 1000
+
+
+def test_dropin_import_surface():
+    import mx_quantization_amd as m
+    mx, funcs = m.install_dropin()
+    from mx import Linear, matmul  # noqa: F401  (deit main.py:36)
+    from mx.elemwise_ops import quantize_elemwise_op  # noqa: F401
+    from mx.mx_ops import quantize_mx_op, _shared_exponents, _reshape_to_blocks, _undo_reshape_to_blocks  # noqa
+    from funcs import (exponent_approximation, elsa_approximation, save_idx_file, save_diff_score_file,  # noqa
+                       diff_idx_analysis, init_analysis_files, _create_structured_orthogonal_matrix,
+                       _modified_gram_schmidt, total_chosen_k, create_file, mismatch_analysis, write_data)
+    assert mx.__name__ == "mx_quantization_amd.mx"
+
+
+def test_reshape_to_blocks_matches_reference_shapes():
+    from mx_quantization_amd.mx.mx_ops import _reshape_to_blocks, _undo_reshape_to_blocks
+    x = torch.randn(2, 3, 197, 72)
+    b, axes, orig, padded = _reshape_to_blocks(x, [-1], 32)
+    assert tuple(b.shape) == (2, 3, 197, 3, 32) and axes == [3]
+    assert torch.equal(_undo_reshape_to_blocks(b, padded, orig, axes), x)
+    b, axes, orig, padded = _reshape_to_blocks(x, [-2], 32)
+    assert tuple(b.shape) == (2, 3, 7, 32, 72)
+    assert torch.equal(_undo_reshape_to_blocks(b, padded, orig, axes), x)
+
+
+def test_specs_semantics():
+    from mx_quantization_amd.mx.specs import MxSpecs, apply_mx_specs, finalize_mx_specs
+    s = apply_mx_specs({"a_elem_format": "int8", "block_size": 32})
+    assert isinstance(s, MxSpecs) and s["scale_bits"] == 0 and s["round"] == "nearest"
+    with pytest.raises(KeyError):
+        apply_mx_specs({"nope": 1})
+    assert finalize_mx_specs({}) is None
+    f = finalize_mx_specs({"a_elem_format": "int8", "round": "floor"})
+    assert f["round_output"] == "floor" and f["a_elem_format_bp"] == "int8"
+
+
+def test_product_refuses_cpu_tensors():
+    import mx_quantization_amd as m
+    from mx_quantization_amd import NativeError
+    x = torch.zeros(2, 64)
+    with pytest.raises(NativeError):
+        m.topk(x, 3)
+    with pytest.raises(NativeError):
+        m.quantize_mx(x)
+    q = torch.zeros(1, 1, 8, 64)
+    with pytest.raises(NativeError):
+        m.mx_topk_attention(q, q, q, 0.125, k_top=4)

@@ -1,0 +1,277 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference-generated
+golden vectors and the CPU oracle.
+
+Bit-exact: MX codes/values/exponents, approximator operands, true and
+approximate scores, top-k indices in torch's CPU order, prune masks.
+Tolerance: the attention output, normwise relative error <= 1e-3 (north star;
+SURVEY.md F7)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mx_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+OUT_TOL = 1e-3
+
+
+def load(name):
+    return np.load(os.path.join(G, name))
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def same(a, b, what=""):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if a.dtype.kind == "f":
+        ok = (a == b) | (np.isnan(a) & np.isnan(b))
+    else:
+        ok = a == b
+    if not ok.all():
+        bad = np.argwhere(~ok)
+        raise AssertionError(f"{what}: {bad.shape[0]}/{ok.size} mismatches, first {bad[:4].tolist()}: "
+                             f"{a[tuple(bad[0])]} vs {b[tuple(bad[0])]}")
+
+
+@pytest.fixture(scope="module")
+def M():
+    import mx_quantization_amd as m
+    return m
+
+
+# ------------------------------------------------------------------ MFMA lane maps
+def test_mfma_i8_lane_maps(M):
+    from mx_quantization_amd.ops import selftest_mfma
+    rng = np.random.default_rng(0)
+    A = rng.integers(-128, 128, (16, 32)).astype(np.int8)
+    B = rng.integers(-128, 128, (32, 16)).astype(np.int8)
+    C = host(selftest_mfma(dev(A), dev(B)))
+    same(C, A.astype(np.int32) @ B.astype(np.int32), "mfma 16x16x32 i8")
+
+
+# ------------------------------------------------------------------ quantization
+@pytest.mark.parametrize("elem,mbits", [("int8", 8), ("int4", 4), ("int2", 2)])
+@pytest.mark.parametrize("rnd", ["nearest", "floor", "even"])
+@pytest.mark.parametrize("flush", [False, True])
+def test_quantize_boundary_vectors(M, elem, mbits, rnd, flush):
+    d = load("quant_kat.npz")
+    y = M.quantize_mx(dev(d["x"]), elem_mbits=mbits, block_size=32, axis=-1, round=rnd, flush=flush)
+    same(host(y), d[f"y_{elem}_{rnd}_{int(flush)}"], f"{elem}/{rnd}/{flush}")
+
+
+def test_quantize_hw_kat_and_scale_bits(M):
+    d = load("quant_kat.npz")
+    same(host(M.quantize_mx(dev(d["hw_x"]), 8, 10, 1)), d["hw_y"], "hw_test")
+    same(host(M.quantize_mx(dev(d["x"]), 8, 32, -1, scale_bits=5)), d["y_int8_nearest_0_sb5"], "scale_bits 5")
+
+
+@pytest.mark.parametrize("bs", [8, 9, 32, 64])
+@pytest.mark.parametrize("ax", [-1, -2, 0])
+def test_quantize_block_sizes_axes(M, bs, ax):
+    d = load("quant_kat.npz")
+    same(host(M.quantize_mx(dev(d["z"]), 8, bs, ax)), d[f"z_bs{bs}_ax{ax}"], f"bs{bs} ax{ax}")
+
+
+def test_shared_exponents_and_bfloat(M):
+    d = load("quant_kat.npz")
+    from mx_quantization_amd.mx.mx_ops import _reshape_to_blocks, _shared_exponents
+    xb, *_ = _reshape_to_blocks(dev(d["x"]), [-1], 32)
+    same(host(_shared_exponents(xb, "max", axes=[-1])), d["sexp_max"], "sexp max")
+    same(host(_shared_exponents(xb, "none", axes=[-1])), d["sexp_none"], "sexp none")
+    same(host(M.quantize_bfloat(dev(d["bf_x"]), 16)), d["bf_y"], "bfloat16")
+
+
+def test_exponent_rule_exhaustive_sample(M):
+    """The device exponent rule on every float32 around every per-binade threshold
+    and a dense sample elsewhere, against torch.log2 on the CPU."""
+    lut = load("exp_lut.npz")
+    parts = []
+    for E in range(1, 255):
+        t = int(min(lut["th_norm"][E], (1 << 23) - 1))
+        parts.append(np.arange((E << 23) | max(0, t - 256), (E << 23) | min(1 << 23, t + 256), dtype=np.uint32))
+    parts.append(np.arange(1, 1 << 23, 97, dtype=np.uint32))
+    parts.append(np.random.default_rng(3).integers(1, 0x7F800000, 1 << 22).astype(np.uint32))
+    b = np.concatenate(parts)
+    x = b.view(np.float32)
+    ref = torch.floor(torch.log2(torch.from_numpy(x))).numpy()
+    got = host(M.shared_exponents(dev(x.reshape(-1, 1)), "none")).reshape(-1)
+    same(got, ref, "floor(log2)")
+
+
+# ------------------------------------------------------------------ top-k order
+@pytest.mark.parametrize("name", ["deit", "deit30", "dit", "cross"])
+def test_topk_ties_exact_order(M, name):
+    d = load("topk_ties.npz")
+    k = int(d[f"{name}_k"])
+    vals, idx = M.topk(dev(d[f"{name}_pred"]), k)
+    same(host(idx).astype(np.int16), d[f"{name}_idx"], name)
+    same(host(vals), np.take_along_axis(d[f"{name}_pred"], host(idx), -1), name + " vals")
+
+
+@pytest.mark.parametrize("n", [120, 197, 256])
+def test_topk_adversarial_rows(M, n):
+    d = load("topk_ties.npz")
+    rows, ks, want = d[f"adv{n}_rows"], d[f"adv{n}_k"], d[f"adv{n}_idx"]
+    for k in np.unique(ks):
+        sel = ks == k
+        _, idx = M.topk(dev(rows[sel]), int(k))
+        same(host(idx).astype(np.int16), want[sel][:, :k], f"n{n} k{k}")
+
+
+@pytest.mark.parametrize("n,k", [(197, 30), (197, 154), (256, 77), (256, 154), (512, 300), (120, 20), (300, 4)])
+def test_topk_depth_limit_fallbacks_and_partial_sort(M, n, k):
+    rows = np.stack([O.antiqsort_row(n, k)] + [np.random.default_rng(i).integers(0, 3, n).astype(np.float32)
+                                                for i in range(7)])
+    _, want = O.topk(rows, k)
+    _, idx = M.topk(dev(rows), k)
+    same(host(idx), want, f"n{n} k{k}")
+
+
+def test_topk_random_small_alphabets_and_specials(M):
+    rng = np.random.default_rng(11)
+    for n in (5, 17, 64, 65, 127, 128, 129, 197, 256, 300, 511, 512):
+        for k in sorted({1, 2, 3, min(n, 20), (n + 1) // 2, n}):
+            rows = rng.integers(-2, 3, (32, n)).astype(np.float32)
+            rows[rows == 2] = np.nan
+            rows[rows == -2] = -0.0
+            _, want = O.topk(rows, k)
+            _, idx = M.topk(dev(rows), k)
+            same(host(idx), want, f"n{n} k{k}")
+
+
+# ------------------------------------------------------------------ approximators
+@pytest.mark.parametrize("mode", ["ex_pred", "partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex"])
+def test_approximator_operands(M, mode):
+    d = load("attn_deit_tiny.npz")
+    M.install_dropin()
+    from funcs import exponent_approximation
+    from mx.specs import apply_mx_specs
+    specs = apply_mx_specs({"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32, "scale_bits": 8,
+                            "bfloat": 32})
+    obj = exponent_approximation(dev(d["q"]), dev(d["k"]), specs)
+    fn = {"ex_pred": obj.exponent_based_sign, "true_ex": obj.exponent_based_sign_leading_ones}.get(
+        mode, getattr(obj, mode, None))
+    aq, ak = fn()
+    same(host(aq)[..., :32, :], d[f"{mode}_k20/aq"], mode + " aq")
+    same(host(ak)[..., :32, :], d[f"{mode}_k20/ak"], mode + " ak")
+
+
+# ------------------------------------------------------------------ fused attention
+CASES = [
+    ("attn_deit_tiny.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
+    ("attn_deit_tiny.npz", "dense", dict(top_k=False)),
+    ("attn_deit_tiny.npz", "trueK_k30", dict(approx=False, k_top=30)),
+    ("attn_deit_tiny.npz", "partial_Q_k20", dict(pred_mode="partial_Q", k_top=20)),
+    ("attn_deit_tiny.npz", "partial_K_k20", dict(pred_mode="partial_K", k_top=20)),
+    ("attn_deit_tiny.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20)),
+    ("attn_deit_tiny.npz", "two_step_leading_ones_k20", dict(pred_mode="two_step_leading_ones", k_top=20)),
+    ("attn_deit_tiny_peaky.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
+    ("attn_dit.npz", "ex_pred_k154", dict(pred_mode="ex_pred", k_top=154)),
+    ("attn_pixart_cross.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20, flush_subnormals=True)),
+    ("attn_pixart_cross.npz", "two_step_leading_ones_k20",
+     dict(pred_mode="two_step_leading_ones", k_top=20, flush_subnormals=True)),
+    ("attn_pixart_cross.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20, flush_subnormals=True)),
+]
+
+
+@pytest.mark.parametrize("fname,tag,kw", CASES, ids=[f"{f[5:-4]}:{t}" for f, t, _ in CASES])
+def test_fused_attention_vs_reference(M, fname, tag, kw):
+    d = load(fname)
+    bias = dev(d["bias"][:, :, None, :]) if "bias" in d.files else None  # (B,1,1,T)
+    out, idx, true_s, pred_s = M.mx_topk_attention(dev(d["q"]), dev(d["k"]), dev(d["v"]), float(d["scale"]),
+                                                   bias=bias, return_scores=True, **kw)
+    torch.cuda.synchronize()
+    same(host(true_s), d["true"], "true scores")
+    if f"{tag}/pred" in d.files:
+        same(host(pred_s), d[f"{tag}/pred"], "approx scores")
+    if f"{tag}/idx" in d.files:
+        same(host(idx), d[f"{tag}/idx"], "top-k idx")
+        T = d["true"].shape[-1]
+        same(O.prune_mask(host(idx), T), O.prune_mask(d[f"{tag}/idx"], T), "prune mask")
+    err = O.normwise_rel_err(host(out), d[f"{tag}/out"])
+    assert err <= OUT_TOL, err
+
+
+def test_fused_attention_strided_qkv_views(M):
+    """q/k/v as permuted views of one packed qkv buffer (deit main.py:87-88, DiT models.py:156-157)."""
+    d = load("attn_deit_tiny.npz")
+    B, H, N, D = d["q"].shape
+    qkv = np.stack([d["q"], d["k"], d["v"]], 0).transpose(1, 3, 0, 2, 4).copy()  # (B,N,3,H,D)
+    t = dev(qkv).permute(2, 0, 3, 1, 4)
+    q, k, v = t[0], t[1], t[2]
+    assert not q.is_contiguous()
+    out, idx = M.mx_topk_attention(q, k, v, float(d["scale"]), k_top=20)
+    same(host(idx), d["ex_pred_k20/idx"], "idx")
+    assert O.normwise_rel_err(host(out), d["ex_pred_k20/out"]) <= OUT_TOL
+
+
+@pytest.mark.parametrize("cfg", ["deit_base", "dit"])
+def test_fused_attention_full_size_vs_oracle(M, cfg):
+    """BASELINE configs at full batch: every head's top-k indices against the oracle's
+    libstdc++ top-k of the kernel's own approximate scores, a sample of heads fully
+    (scores, indices, output) against the oracle."""
+    if cfg == "deit_base":
+        B, H, N, D, k, scale = 256, 12, 197, 64, 20, 64 ** -0.5
+    else:
+        B, H, N, D, k, scale = 64, 16, 256, 72, 154, 72 ** -0.5
+    q, kk, v = (torch.from_numpy(np.random.default_rng(s).standard_normal((B, H, N, D), dtype=np.float32)).cuda()
+                for s in (0, 1, 2))
+    out, idx, true_s, pred_s = M.mx_topk_attention(q, kk, v, scale, k_top=k, return_scores=True)
+    pred_h = host(pred_s)
+    _, want = O.topk(pred_h.reshape(-1, N), k)
+    same(host(idx).reshape(-1, k), want, "idx (all heads)")
+    for b in (0, B // 2, B - 1):
+        r = O.attention(host(q[b:b + 1]), host(kk[b:b + 1]), host(v[b:b + 1]), scale, k_top=k)
+        same(host(true_s[b:b + 1]), r["true"], "true")
+        same(pred_h[b:b + 1], r["pred"], "pred")
+        same(host(idx[b:b + 1]), r["idx"], "idx")
+        assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
+
+
+def test_pixart_cross_full_batch(M):
+    B, H, N, T, D, k = 8, 16, 256, 120, 72, 20
+    rng = np.random.default_rng(0)
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    bias = np.where(np.arange(T) < 60, 0.0, -10000.0).astype(np.float32)[None, None, None, :].repeat(B, 0)
+    for mode in ("MXINT4", "two_step_leading_ones"):
+        out, idx = M.mx_topk_attention(dev(q), dev(kk), dev(v), 1 / np.sqrt(72), k_top=k, pred_mode=mode,
+                                       bias=dev(bias), flush_subnormals=True)
+        r = O.attention(q[:2], kk[:2], v[:2], 1 / np.sqrt(72), k_top=k, pred_mode=mode, bias=bias[:2], flush=True)
+        same(host(idx)[:2], r["idx"], mode)
+        assert O.normwise_rel_err(host(out)[:2], r["out"]) <= OUT_TOL
+
+
+# ------------------------------------------------------------------ mx.matmul / Linear drop-in
+def test_mx_matmul_dropin(M):
+    d = load("attn_deit_tiny.npz")
+    mx, _ = M.install_dropin()
+    specs = {"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32, "scale_bits": 8, "bfloat": 32}
+    q, k = dev(d["q"]), dev(d["k"])
+    t = mx.matmul(q, k.transpose(-2, -1), mx_specs=specs) * float(d["scale"])
+    same(host(t), d["true"], "mx.matmul QK^T")
+    a = np.random.default_rng(5).standard_normal((4, 37, 100), dtype=np.float32)
+    b = np.random.default_rng(6).standard_normal((4, 100, 45), dtype=np.float32)
+    same(host(mx.matmul(dev(a), dev(b), mx_specs=specs)), O.mx_matmul(a, b), "ragged mx.matmul")
+
+
+def test_linear_dropin(M):
+    mx, _ = M.install_dropin()
+    specs = {"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32, "scale_bits": 8, "bfloat": 32}
+    lin = mx.Linear(96, 80, bias=True, mx_specs=specs).cuda()
+    x = torch.randn(2, 7, 96, device="cuda")
+    y = lin(x)
+    want = O.mx_matmul(host(x), host(lin.weight).T) + host(lin.bias)
+    assert np.max(np.abs(host(y) - want)) <= 1e-5 * max(1.0, np.abs(want).max())
