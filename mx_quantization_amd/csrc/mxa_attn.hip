@@ -99,8 +99,9 @@ __global__ __launch_bounds__(256) void scores_topk_kernel(ScoresArgs a) {
 
   // ---- per row: top-k, softmax, scatter, MX-quantize P along keys ----------
   TopkLds sc;
-  sc.a = scr_base + (size_t)wave * 2 * (64 * S);
+  sc.a = scr_base + (size_t)wave * (2 * 64 * S + kTopkStack / 2);
   sc.b = sc.a + 64 * S;
+  sc.stk = reinterpret_cast<int*>(sc.b + 64 * S);
   for (int r = wave; r < rows_valid; r += 4) {
     const int64_t grow = qrow0 + r;
     float* trow = tileT + r * a.tpad;
@@ -251,8 +252,9 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(TopkArgs a) {
   const int64_t row = (int64_t)blockIdx.x * 4 + wave;
   if (row >= a.rows) return;  // wave-uniform
   TopkLds sc;
-  sc.a = reinterpret_cast<uint64_t*>(smem) + (size_t)wave * 2 * (64 * S);
+  sc.a = reinterpret_cast<uint64_t*>(smem) + (size_t)wave * (2 * 64 * S + kTopkStack / 2);
   sc.b = sc.a + 64 * S;
+  sc.stk = reinterpret_cast<int*>(sc.b + 64 * S);
   const float* src = a.vals + row * a.ld;
   WaveRow<S> w;
   w.lane = lane;
@@ -387,7 +389,8 @@ extern "C" int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p) {
 
 template <int S>
 static int launch_scores(const ScoresArgs& sa, int BH, int N, hipStream_t stream) {
-  const size_t lds = (size_t)2 * kRowsPerWG * sa.tpad * sizeof(float) + (size_t)4 * 2 * 64 * S * sizeof(uint64_t);
+  const size_t lds = (size_t)2 * kRowsPerWG * sa.tpad * sizeof(float) +
+                     (size_t)4 * (2 * 64 * S + kTopkStack / 2) * sizeof(uint64_t);
   dim3 grid((unsigned)((N + kRowsPerWG - 1) / kRowsPerWG), (unsigned)BH);
   if (lds > 65536 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&scores_topk_kernel<S>),
@@ -527,7 +530,7 @@ extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream,
 
 template <int S>
 static int launch_topk(const TopkArgs& ta, hipStream_t stream) {
-  const size_t lds = (size_t)4 * 2 * 64 * S * sizeof(uint64_t);
+  const size_t lds = (size_t)4 * (2 * 64 * S + kTopkStack / 2) * sizeof(uint64_t);
   hipLaunchKernelGGL(topk_rows_kernel<S>, dim3((unsigned)((ta.rows + 3) / 4)), dim3(256), lds, stream, ta);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }

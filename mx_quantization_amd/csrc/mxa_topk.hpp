@@ -39,13 +39,25 @@ __device__ __forceinline__ uint64_t pack_ki(uint32_t key, uint32_t idx) {
   return ((uint64_t)key << 32) | idx;
 }
 
-// per-wave LDS scratch, 2*nmax uint64 entries
+// per-wave LDS scratch
 struct TopkLds {
   uint64_t* a;  // nmax entries
   uint64_t* b;  // nmax entries
+  int* stk;     // kTopkStack entries (introsort's pending segments)
 };
+constexpr int kTopkStack = 24;  // >= 2*lg(511) + 1 pending segments
 
 __device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
+
+// bits [lo, hi) of a 64-bit mask, lo/hi clamped to [0, 64]
+__device__ __forceinline__ uint64_t range_mask(int lo, int hi) {
+  lo = lo < 0 ? 0 : (lo > 64 ? 64 : lo);
+  hi = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
+  if (hi <= lo) return 0ull;
+  const uint64_t up = hi == 64 ? ~0ull : ((1ull << hi) - 1ull);
+  const uint64_t dn = (1ull << lo) - 1ull;
+  return up & ~dn;
+}
 
 template <int S>
 struct WaveRow {
@@ -53,106 +65,134 @@ struct WaveRow {
   uint32_t idx[S];
   int lane;
 
+  // value at uniform position p: one readlane per slot, selected without branches
   __device__ __forceinline__ uint32_t get_key(int p) const {
     const int sl = p >> 6, ln = p & 63;
-    uint32_t v = 0;
+    uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)key[0], ln);
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (s == sl) v = (uint32_t)__builtin_amdgcn_readlane((int)key[s], ln);
+    for (int s = 1; s < S; ++s) {
+      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)key[s], ln);
+      v = sl == s ? w : v;
+    }
     return v;
   }
   __device__ __forceinline__ uint32_t get_idx(int p) const {
     const int sl = p >> 6, ln = p & 63;
-    uint32_t v = 0;
+    uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)idx[0], ln);
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (s == sl) v = (uint32_t)__builtin_amdgcn_readlane((int)idx[s], ln);
+    for (int s = 1; s < S; ++s) {
+      const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)idx[s], ln);
+      v = sl == s ? w : v;
+    }
     return v;
   }
   __device__ __forceinline__ void set(int p, uint32_t k, uint32_t i) {
     const int sl = p >> 6, ln = p & 63;
+    const bool me = lane == ln;
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (s == sl && lane == ln) {
-        key[s] = k;
-        idx[s] = i;
-      }
-  }
-  __device__ __forceinline__ void swap_pos(int p, int q) {
-    if (p == q) return;
-    const uint32_t kp = get_key(p), ip = get_idx(p), kq = get_key(q), iq = get_idx(q);
-    set(p, kq, iq);
-    set(q, kp, ip);
+    for (int s = 0; s < S; ++s) {
+      const bool hit = me && s == sl;
+      key[s] = hit ? k : key[s];
+      idx[s] = hit ? i : idx[s];
+    }
   }
 
   // libstdc++ __unguarded_partition_pivot(first, last) with cmp = greater.
   __device__ int partition_pivot(int first, int last, const TopkLds& sc) {
     const int mid = first + (last - first) / 2;
-    const int a = first + 1, b = mid, c = last - 1;
-    const uint32_t ka = get_key(a), kb = get_key(b), kc = get_key(c);
-    int m;  // __move_median_to_first(first, a, b, c)
+    const uint32_t ka = get_key(first + 1), kb = get_key(mid), kc = get_key(last - 1);
+    int m;  // __move_median_to_first(first, first+1, mid, last-1)
     if (ka > kb) {
-      if (kb > kc) m = b;
-      else if (ka > kc) m = c;
-      else m = a;
-    } else if (ka > kc) m = a;
-    else if (kb > kc) m = c;
-    else m = b;
-    swap_pos(first, m);
-    const uint32_t p = get_key(first);
+      if (kb > kc) m = mid;
+      else if (ka > kc) m = last - 1;
+      else m = first + 1;
+    } else if (ka > kc) m = first + 1;
+    else if (kb > kc) m = last - 1;
+    else m = mid;
+    const uint32_t p = m == first + 1 ? ka : (m == mid ? kb : kc);
+    {  // iter_swap(first, m)
+      const uint32_t kf = get_key(first), jf = get_idx(first), jm = get_idx(m);
+      set(first, p, jm);
+      set(m, kf, jf);
+    }
     const int s0 = first >> 6, s1 = (last - 1) >> 6;
     uint64_t L[S], R[S];
-    bool lst[S], rst[S];
-    int cl_before[S], cr_before[S];
+    int cl[S], cr[S];
     int totL = 0, totR = 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pos = s * 64 + lane;
-      const bool in_r = (s >= s0 && s <= s1) && pos >= first && pos < last;
-      lst[s] = in_r && pos > first && !(key[s] > p);
-      rst[s] = in_r && !(p > key[s]);
-      L[s] = __ballot(lst[s]);
-      R[s] = __ballot(rst[s]);
-      cl_before[s] = totL;
-      cr_before[s] = totR;
+      L[s] = R[s] = 0ull;
+      cl[s] = totL;
+      cr[s] = totR;
+      if (s < s0 || s > s1) continue;  // uniform: slot outside the segment
+      const uint64_t rr = range_mask(first - 64 * s, last - 64 * s);
+      const uint64_t rl = range_mask(first + 1 - 64 * s, last - 64 * s);
+      L[s] = __ballot(key[s] <= p) & rl;  // left stop:  !(a > p)
+      R[s] = __ballot(key[s] >= p) & rr;  // right stop: !(p > a)
       totL += __popcll(L[s]);
       totR += __popcll(R[s]);
     }
     bool swl[S], swr[S];
     int rank[S];
+    int msw = 0;
+    uint64_t SWL[S], SWR[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int A = cl_before[s] + mbcnt(L[s]);
-      const int Bgt = totR - cr_before[s] - mbcnt(R[s]) - (rst[s] ? 1 : 0);
-      swl[s] = lst[s] && Bgt > A;
-      swr[s] = rst[s] && A > Bgt;
+      swl[s] = swr[s] = false;
+      rank[s] = 0;
+      SWL[s] = SWR[s] = 0ull;
+      if (s < s0 || s > s1) continue;
+      const bool isl = (L[s] >> lane) & 1ull, isr = (R[s] >> lane) & 1ull;
+      const int A = cl[s] + mbcnt(L[s]);
+      const int Bgt = totR - cr[s] - mbcnt(R[s]) - (isr ? 1 : 0);
+      swl[s] = isl && Bgt > A;
+      swr[s] = isr && A > Bgt;
       rank[s] = swl[s] ? A : Bgt;
-      if (swl[s]) sc.a[rank[s]] = pack_ki(key[s], idx[s]);
-      if (swr[s]) sc.b[rank[s]] = pack_ki(key[s], idx[s]);
+      SWL[s] = __ballot(swl[s]);
+      SWR[s] = __ballot(swr[s]);
+      msw += __popcll(SWL[s]);
     }
-    wave_lds_sync();
-    int c1 = 1 << 30, c2 = -1, msw = 0;
+    if (msw > 0) {  // exchange the t-th swapping left stop with the t-th swapping right stop
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s < s0 || s > s1) continue;
+        if (swl[s]) sc.a[rank[s]] = pack_ki(key[s], idx[s]);
+        if (swr[s]) sc.b[rank[s]] = pack_ki(key[s], idx[s]);
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s < s0 || s > s1) continue;
+        if (swl[s] || swr[s]) {
+          const uint64_t v = swl[s] ? sc.b[rank[s]] : sc.a[rank[s]];
+          key[s] = (uint32_t)(v >> 32);
+          idx[s] = (uint32_t)v;
+        }
+      }
+      wave_lds_sync();
+    }
+    // cut = min(first non-swapping left stop, lowest swapping right stop | last)
+    int c1 = 1 << 30, c2 = last;
+    bool f1 = false, f2 = msw == 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (swl[s] || swr[s]) {
-        const uint64_t v = swl[s] ? sc.b[rank[s]] : sc.a[rank[s]];
-        key[s] = (uint32_t)(v >> 32);
-        idx[s] = (uint32_t)v;
+      if (s < s0 || s > s1) continue;
+      const uint64_t nsl = L[s] & ~SWL[s];
+      if (!f1 && nsl) {
+        c1 = 64 * s + __ffsll((unsigned long long)nsl) - 1;
+        f1 = true;
       }
-      const uint64_t nsl = __ballot(lst[s] && !swl[s]);
-      const uint64_t swrb = __ballot(swr[s]);
-      msw += __popcll(swrb);
-      if (nsl && c1 == (1 << 30)) c1 = s * 64 + __ffsll((unsigned long long)nsl) - 1;
-      if (swrb && c2 < 0) c2 = s * 64 + __ffsll((unsigned long long)swrb) - 1;
+      if (!f2 && SWR[s]) {
+        c2 = 64 * s + __ffsll((unsigned long long)SWR[s]) - 1;
+        f2 = true;
+      }
     }
-    wave_lds_sync();
-    if (msw == 0) c2 = last;
     return c1 < c2 ? c1 : c2;
   }
 
-  // Stable sort (by key, descending) of the segment each lane's position belongs to:
-  // lanes with seg_lo[s] < seg_hi[s] participate.  Segments must be disjoint.
-  __device__ void stable_sort_segments(const int (&seg_lo)[S], const int (&seg_hi)[S], int n,
+  // Stable sort (key descending) of the segment [lo[s], hi[s]) each position belongs
+  // to (segments of at most `maxlen` elements, disjoint; lo == hi: not in a segment).
+  __device__ void stable_sort_segments(const int (&lo)[S], const int (&hi)[S], int n, int maxlen,
                                        const TopkLds& sc) {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -160,25 +200,28 @@ struct WaveRow {
       if (pos < n) sc.a[pos] = pack_ki(key[s], idx[s]);
     }
     wave_lds_sync();
+    int r[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const int pos = s * 64 + lane;
-      if (seg_lo[s] < seg_hi[s]) {
-        int r = 0;
-        const uint32_t mk = key[s];
-        for (int j = seg_lo[s]; j < seg_hi[s]; ++j) {
-          const uint32_t kj = (uint32_t)(sc.a[j] >> 32);
-          r += (kj > mk || (kj == mk && j < pos)) ? 1 : 0;
+    for (int s = 0; s < S; ++s) r[s] = 0;
+    for (int j = 0; j < maxlen; ++j) {  // all slots' loads in flight together
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int q = lo[s] + j;
+        if (q < hi[s]) {
+          const int pos = s * 64 + lane;
+          const uint32_t kj = (uint32_t)(sc.a[q] >> 32);
+          r[s] += (kj > key[s] || (kj == key[s] && q < pos)) ? 1 : 0;
         }
-        sc.b[seg_lo[s] + r] = pack_ki(key[s], idx[s]);
       }
     }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if (lo[s] < hi[s]) sc.b[lo[s] + r[s]] = pack_ki(key[s], idx[s]);
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (seg_lo[s] < seg_hi[s]) {
-        const int pos = s * 64 + lane;
-        const uint64_t v = sc.b[pos];
+      if (lo[s] < hi[s]) {
+        const uint64_t v = sc.b[s * 64 + lane];
         key[s] = (uint32_t)(v >> 32);
         idx[s] = (uint32_t)v;
       }
@@ -306,7 +349,7 @@ __device__ void wave_topk(WaveRow<S>& w, int n, int k, const TopkLds& sc) {
       if (cut <= nth) first = cut;
       else last = cut;
     }
-    if (!fell_back && last - first > 1) {
+    if (!fell_back && last - first > 1) {  // __insertion_sort(first, last): <= 3 elements
       int lo[S], hi[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -315,7 +358,7 @@ __device__ void wave_topk(WaveRow<S>& w, int n, int k, const TopkLds& sc) {
         lo[s] = in ? first : 0;
         hi[s] = in ? last : 0;
       }
-      w.stable_sort_segments(lo, hi, n, sc);
+      w.stable_sort_segments(lo, hi, n, last - first, sc);
     }
   }
   // ---- std::sort(begin, begin+k-1): __introsort_loop + final insertion sort --
@@ -324,22 +367,24 @@ __device__ void wave_topk(WaveRow<S>& w, int n, int k, const TopkLds& sc) {
   int lo[S], hi[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) lo[s] = hi[s] = 0;
-  // explicit stack of pending segments (cut, last, depth); order is irrelevant
-  // because segments are disjoint.  Depth of the stack <= 2*lg(m) + 1 < 20.
-  int st_f[20], st_l[20], st_d[20];
+  // pending segments (cut, last, depth) packed 10|10|6 bits; segments are disjoint,
+  // so the order they are processed in does not matter
   int sp = 0;
-  st_f[0] = 0;
-  st_l[0] = m;
-  st_d[0] = 2 * ilog2(m);
-  sp = 1;
+  auto push = [&](int f, int l, int d) {
+    if (sp < kTopkStack) sc.stk[sp] = f | (l << 10) | (d << 20);
+    ++sp;
+  };
+  push(0, m, 2 * ilog2(m));
   while (sp > 0) {
+    wave_lds_sync();
     --sp;
-    const int f = st_f[sp];
-    int l = st_l[sp];
-    int d = st_d[sp];
+    const int e = sc.stk[sp];
+    const int f = e & 1023;
+    int l = (e >> 10) & 1023;
+    int d = e >> 20;
     bool heaped = false;
     while (l - f > 16) {
-      if (d == 0) {  // std::__partial_sort(f, l, l): heapsort, already in final order
+      if (d == 0) {  // std::__partial_sort(f, l, l): heapsort, leaves [f, l) in final order
         w.to_lds(sc.a, n);
         wave_lds_sync();
         if (w.lane == 0) {
@@ -354,26 +399,20 @@ __device__ void wave_topk(WaveRow<S>& w, int n, int k, const TopkLds& sc) {
       }
       --d;
       const int cut = w.partition_pivot(f, l, sc);
-      if (sp < 20) {  // bound: <= 2*lg(m)+1 pending segments
-        st_f[sp] = cut;
-        st_l[sp] = l;
-        st_d[sp] = d;
-        ++sp;
-      }
+      push(cut, l, d);
       l = cut;
     }
     if (!heaped && l - f > 1) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int pos = s * 64 + w.lane;
-        if (pos >= f && pos < l) {
-          lo[s] = f;
-          hi[s] = l;
-        }
+        const bool in = pos >= f && pos < l;
+        lo[s] = in ? f : lo[s];
+        hi[s] = in ? l : hi[s];
       }
     }
   }
-  w.stable_sort_segments(lo, hi, n, sc);
+  w.stable_sort_segments(lo, hi, n, 16, sc);
 }
 
 }  // namespace mxa
