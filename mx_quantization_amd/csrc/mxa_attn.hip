@@ -13,7 +13,11 @@
 //   workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859.
 #include "mxa_kernels.hpp"
 #include "mxa_topk.hpp"
+#include "mxa_topk_lds.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 namespace mxa {
@@ -35,12 +39,113 @@ struct ScoresArgs {
   int16_t* ps;  // [B*H*N][ntb]
 };
 
+// Row tail shared by the fused kernels, one wave per row:
+// top-k in torch's CPU order (TopKImpl.h:45-86) on the approximate scores,
+// softmax over the kept true scores, scatter, MX quantization of P along keys.
+// trow / prow: the row's true and approximate scores in LDS (tpad floats each);
+// prow is reused for the dense P row.
+template <int S>
+__device__ void finish_row(const ScoresArgs& a, int64_t grow, float* trow, float* prow, const TopkLdsV2& sc,
+                           int lane) {
+  float pv[S];
+  if (a.top_k) {
+    const float* src = a.approx ? prow : trow;
+    for (int pos = lane; pos < a.T; pos += 64) sc.A[pos] = pack_ki(order_key(src[pos]), (uint32_t)pos);
+    wave_lds_sync();
+    lds_topk<S>(sc, a.T, a.k_top, lane);
+    uint32_t widx[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      widx[s] = pos < a.k_top ? (uint32_t)sc.A[pos] : 0u;
+    }
+    // vals = true.gather(idx); softmax(vals); zeros.scatter_(idx, softmax)
+    float v[S];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      v[s] = -INFINITY;
+      if (pos < a.k_top) {
+        if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)widx[s];
+        v[s] = trow[widx[s]];
+        mx = fmaxf(mx, v[s]);
+      }
+    }
+    mx = wave_max_f32(mx);
+    float sum = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      v[s] = pos < a.k_top ? expf(v[s] - mx) : 0.0f;
+      sum += v[s];
+    }
+    sum = wave_sum_f32(sum);
+    wave_lds_sync();
+    for (int pos = lane; pos < a.tpad; pos += 64) prow[pos] = 0.0f;
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      if (pos < a.k_top) prow[widx[s]] = v[s] / sum;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      pv[s] = pos < a.tpad ? prow[pos] : 0.0f;
+    }
+  } else {
+    // dense: attn = softmax(true) (blocks excluded from top-k)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      pv[s] = pos < a.T ? trow[pos] : -INFINITY;
+      mx = fmaxf(mx, pv[s]);
+    }
+    mx = wave_max_f32(mx);
+    float sum = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      pv[s] = pos < a.T ? expf(pv[s] - mx) : 0.0f;
+      sum += pv[s];
+    }
+    sum = wave_sum_f32(sum);
+#pragma unroll
+    for (int s = 0; s < S; ++s) pv[s] = pv[s] / sum;
+  }
+  // P -> MXINT8 along keys (matmul(attn, v): quantize_mx_op(axes=[-1]), matmul.py:68-76)
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = s * 64 + lane;
+    if (s * 64 >= a.tpad) break;
+    const float x = round_bfloat(pv[s], a.bfloat, kRoundNearest, 1);
+    uint32_t mb = __float_as_uint(x) & 0x7FFFFFFFu;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t w2 = (uint32_t)__shfl_xor((int)mb, o, 32);
+      mb = w2 > mb ? w2 : mb;
+    }
+    int e_raw;
+    const int es = scale_exponent(mb, 127, &e_raw);
+    float xv = x;
+    if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
+    const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+    if (pos < a.tpad) {
+      a.pc[grow * a.tpad + pos] = (int8_t)code;
+      if ((lane & 31) == 0) a.ps[grow * a.ntb + (pos >> 5)] = exp_to16(es == kExpNaN ? kExpNaN : es - 6);
+    }
+  }
+}
+
 template <int S>
 __global__ __launch_bounds__(256) void scores_topk_kernel(ScoresArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* tileT = reinterpret_cast<float*>(smem);   // [16][tpad] true scores (then P)
   float* tileP = tileT + kRowsPerWG * a.tpad;       // [16][tpad] approximate scores
-  uint64_t* scr_base = reinterpret_cast<uint64_t*>(tileP + kRowsPerWG * a.tpad);
+  unsigned char* scr_base = reinterpret_cast<unsigned char*>(tileP + kRowsPerWG * a.tpad);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.y;
   const int row0 = blockIdx.x * kRowsPerWG;
@@ -98,105 +203,230 @@ __global__ __launch_bounds__(256) void scores_topk_kernel(ScoresArgs a) {
   __syncthreads();
 
   // ---- per row: top-k, softmax, scatter, MX-quantize P along keys ----------
-  TopkLds sc;
-  sc.a = scr_base + (size_t)wave * (2 * 64 * S + kTopkStack / 2);
-  sc.b = sc.a + 64 * S;
-  sc.stk = reinterpret_cast<int*>(sc.b + 64 * S);
-  for (int r = wave; r < rows_valid; r += 4) {
-    const int64_t grow = qrow0 + r;
-    float* trow = tileT + r * a.tpad;
-    float* prow = tileP + r * a.tpad;
-    float pv[S];
-    if (a.top_k) {
-      WaveRow<S> w;
-      w.lane = lane;
-      const float* src = a.approx ? prow : trow;
+  const TopkLdsV2 sc = carve_topk(scr_base + (size_t)wave * topk_scratch_bytes(S), S);
+  for (int r = wave; r < rows_valid; r += 4)
+    finish_row<S>(a, qrow0 + r, tileT + r * a.tpad, tileP + r * a.tpad, sc, lane);
+}
+
+// ---- row-oriented fused scores + top-k: one wave per query row -------------
+// A workgroup of kRowsWaves waves takes the rows of one head.  The head's key
+// operand (approximator codes for the approximate scores, or the MX codes when
+// the keys are true scores) is staged once in LDS; every wave then computes its
+// row's T scores with v_dot4_i32_i8 per 32-element MX block and an exact fp64
+// block epilogue (the same floats scaled_tile gives), writes them
+// as order keys straight into its LDS top-k array, runs lds_topk, and computes
+// the true scores of the kept keys only.  Softmax, scatter and the MX
+// quantization of P along keys follow; P leaves as MXINT8 codes for pv_kernel.
+constexpr int kRowsWaves = 8;
+constexpr int kMaxNB = 4;  // head dim <= 128
+
+struct RowsArgs {
+  ScoresArgs s;
+  int kst;          // LDS row stride of the key operand table (dpad + 16: conflict-free b128 reads)
+  int key_is_true;  // table holds the K MX codes: the row values are true scores
+  int rows_per_wg;
+};
+
+__host__ __device__ inline size_t rows_wave_bytes(int S, int tpad) {
+  return topk_scratch_bytes(S) + (size_t)tpad * 4 + 64;
+}
+__host__ __device__ inline size_t rows_lds_bytes(int T, int kst, int nbd, int S, int tpad) {
+  return (size_t)T * kst + (((size_t)T * nbd * 2 + 15) & ~(size_t)15) + (size_t)kRowsWaves * rows_wave_bytes(S, tpad);
+}
+
+// uniform row of int8 codes (dpad bytes) -> registers, blocks < nbd
+__device__ __forceinline__ void load_row_codes(const int8_t* src, int nbd, uint32_t (&w)[kMaxNB * 8]) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        w.key[s] = pos < a.T ? order_key(src[pos]) : 0u;
-        w.idx[s] = (uint32_t)pos;
-      }
-      wave_topk<S>(w, a.T, a.k_top, sc);
-      // vals = true.gather(idx); softmax(vals); zeros.scatter_(idx, softmax)
-      float v[S];
-      float mx = -INFINITY;
+  for (int b = 0; b < kMaxNB; ++b) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        v[s] = -INFINITY;
-        if (pos < a.k_top) {
-          if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)w.idx[s];
-          v[s] = trow[w.idx[s]];
-          mx = fmaxf(mx, v[s]);
-        }
-      }
-      mx = wave_max_f32(mx);
-      float sum = 0.0f;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        v[s] = pos < a.k_top ? expf(v[s] - mx) : 0.0f;
-        sum += v[s];
-      }
-      sum = wave_sum_f32(sum);
-      wave_lds_sync();
-      for (int pos = lane; pos < a.tpad; pos += 64) prow[pos] = 0.0f;
-      wave_lds_sync();
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        if (pos < a.k_top) prow[w.idx[s]] = v[s] / sum;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        pv[s] = pos < a.tpad ? prow[pos] : 0.0f;
-      }
-    } else {
-      // dense: attn = softmax(true) (blocks excluded from top-k)
-      float mx = -INFINITY;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        pv[s] = pos < a.T ? trow[pos] : -INFINITY;
-        mx = fmaxf(mx, pv[s]);
-      }
-      mx = wave_max_f32(mx);
-      float sum = 0.0f;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        pv[s] = pos < a.T ? expf(pv[s] - mx) : 0.0f;
-        sum += pv[s];
-      }
-      sum = wave_sum_f32(sum);
-#pragma unroll
-      for (int s = 0; s < S; ++s) pv[s] = pv[s] / sum;
+    for (int c = 0; c < 2; ++c) {
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (b < nbd) v = *reinterpret_cast<const uint4*>(src + 32 * b + 16 * c);
+      // the row is wave-uniform: keep it in SGPRs (v_dot4 takes one scalar operand)
+      w[8 * b + 4 * c] = __builtin_amdgcn_readfirstlane(v.x);
+      w[8 * b + 4 * c + 1] = __builtin_amdgcn_readfirstlane(v.y);
+      w[8 * b + 4 * c + 2] = __builtin_amdgcn_readfirstlane(v.z);
+      w[8 * b + 4 * c + 3] = __builtin_amdgcn_readfirstlane(v.w);
     }
-    // P -> MXINT8 along keys (matmul(attn, v): quantize_mx_op(axes=[-1]), matmul.py:68-76)
+  }
+}
+
+// fl32(exact sum_b I_b * scale_b): EXP scale 2^(sa + sb), MUL scale sa * sb / 4096
+template <bool MUL>
+__device__ __forceinline__ float block_scaled_dot(const uint32_t (&qw)[kMaxNB * 8], const int (&qs)[kMaxNB],
+                                                  const int8_t* krow, const int16_t* ks, int nbd) {
+  double acc = 0.0;
+  bool nan = false;
+#pragma unroll
+  for (int b = 0; b < kMaxNB; ++b) {
+    if (b < nbd) {
+      const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
+      int I = 0;
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 0], (int)x0.x, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 1], (int)x0.y, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 2], (int)x0.z, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 3], (int)x0.w, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 4], (int)x1.x, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 5], (int)x1.y, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 6], (int)x1.z, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 7], (int)x1.w, I, false);
+      const int e = exp_from16(ks[b]);
+      if (e == kExpNaN || qs[b] == kExpNaN) nan = true;
+      else if (MUL) acc += (double)I * (double)(qs[b] * e) * (1.0 / 4096.0);
+      else acc += (double)I * pow2d(qs[b] + e);
+    }
+  }
+  return nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+}
+
+template <int S, bool MUL, bool TOPK>
+__global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs ra) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const ScoresArgs& a = ra.s;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.y;
+  const int T = a.T, nbd = a.nbd;
+  const int b_ = bh / a.H, h_ = bh % a.H;
+  int8_t* tab = reinterpret_cast<int8_t*>(smem);                         // [T][kst]
+  int16_t* tsc = reinterpret_cast<int16_t*>(smem + (size_t)T * ra.kst);  // [T][nbd]
+  unsigned char* wbase = smem + (size_t)T * ra.kst + (((size_t)T * nbd * 2 + 15) & ~(size_t)15) +
+                         (size_t)wave * rows_wave_bytes(S, a.tpad);
+  const TopkLdsV2 sc = carve_topk(wbase, S);
+  float* rowbuf = reinterpret_cast<float*>(wbase + topk_scratch_bytes(S));  // [tpad]
+  uint32_t* bm = reinterpret_cast<uint32_t*>(rowbuf + a.tpad);               // [16]
+
+  // ---- stage the head's key operand ----------------------------------------
+  const int8_t* ksrc = (ra.key_is_true ? a.kc : a.kop) + (int64_t)bh * T * a.dpad;
+  const int16_t* ssrc = (ra.key_is_true ? a.ksT : a.ksA) + (int64_t)bh * T * nbd;
+  const int cpr = a.dpad / 16;
+  for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+    const int j = i / cpr, c = i - j * cpr;
+    *reinterpret_cast<uint4*>(tab + (size_t)j * ra.kst + 16 * c) =
+        *reinterpret_cast<const uint4*>(ksrc + (int64_t)j * a.dpad + 16 * c);
+  }
+  for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tsc[i] = ssrc[i];
+  __syncthreads();
+
+  const int64_t kb = (int64_t)bh * T;
+  const int r0 = blockIdx.x * ra.rows_per_wg;
+  const int r1 = min(a.N, r0 + ra.rows_per_wg);
+  for (int r = r0 + wave; r < r1; r += kRowsWaves) {
+    const int64_t grow = (int64_t)bh * a.N + r;
+    const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
+    // ---- the row's T values (approximate scores, or true scores) -----------
+    uint32_t qw[kMaxNB * 8];
+    int qs[kMaxNB];
+    load_row_codes((ra.key_is_true ? a.qc : a.qop) + grow * a.dpad, nbd, qw);
+#pragma unroll
+    for (int b = 0; b < kMaxNB; ++b)
+      qs[b] = b < nbd ? exp_from16((ra.key_is_true ? a.qsT : a.qsA)[grow * nbd + b]) : 0;
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      const int j = 64 * s + lane;
+      if (j < T) {
+        float v = block_scaled_dot<MUL>(qw, qs, tab + (size_t)j * ra.kst, tsc + (size_t)j * nbd, nbd);
+        const float bv = brow ? brow[(int64_t)j * a.bs3] : 0.0f;
+        if (ra.key_is_true) {
+          // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)   (matmul.py:88-91, caller)
+          v = round_bfloat(v, a.bfloat, kRoundNearest, 1) * a.scale;
+          if (brow) v = v + bv;
+          if (a.true_out) a.true_out[grow * T + j] = v;
+        } else {
+          if (brow) v = v + bv;
+          if (a.pred_out) a.pred_out[grow * T + j] = v;
+        }
+        if (TOPK) sc.A[j] = pack_ki(order_key(v), (uint32_t)j);
+        else rowbuf[j] = v;
+      }
+    }
+    wave_lds_sync();
+
+    if constexpr (!TOPK) {  // dense: softmax over every key (finish_row's dense branch)
+      finish_row<S>(a, grow, rowbuf, rowbuf, sc, lane);
+      wave_lds_sync();
+      continue;
+    }
+    lds_topk<S>(sc, T, a.k_top, lane);
+    // ---- vals = true.gather(idx); softmax(vals) ------------------------------
+    // true scores of the kept keys only (and of every key for the debug output)
+    uint32_t tw[kMaxNB * 8];
+    int ts[kMaxNB];
+    load_row_codes(a.qc + grow * a.dpad, nbd, tw);
+#pragma unroll
+    for (int b = 0; b < kMaxNB; ++b) ts[b] = b < nbd ? exp_from16(a.qsT[grow * nbd + b]) : 0;
+    auto true_score = [&](int j) {
+      float t = block_scaled_dot<false>(tw, ts, a.kc + (kb + j) * a.dpad, a.ksT + (kb + j) * nbd, nbd);
+      t = round_bfloat(t, a.bfloat, kRoundNearest, 1) * a.scale;
+      if (brow) t = t + brow[(int64_t)j * a.bs3];
+      return t;
+    };
+    if (a.true_out && !ra.key_is_true)
+      for (int j = lane; j < T; j += 64) a.true_out[grow * T + j] = true_score(j);
+    float v[S];
+    uint32_t ix[S];
+    float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pos = s * 64 + lane;
-      if (s * 64 >= a.tpad) break;
-      const float x = round_bfloat(pv[s], a.bfloat, kRoundNearest, 1);
-      uint32_t mb = __float_as_uint(x) & 0x7FFFFFFFu;
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        const uint32_t w2 = (uint32_t)__shfl_xor((int)mb, o, 32);
-        mb = w2 > mb ? w2 : mb;
+      const int pos = 64 * s + lane;
+      v[s] = -INFINITY;
+      ix[s] = 0u;
+      if (pos < a.k_top) {
+        ix[s] = (uint32_t)sc.A[pos];
+        if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
+        v[s] = true_score((int)ix[s]);
+        mx = fmaxf(mx, v[s]);
       }
-      int e_raw;
-      const int es = scale_exponent(mb, 127, &e_raw);
-      float xv = x;
-      if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
-      const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
-      if (pos < a.tpad) {
-        a.pc[grow * a.tpad + pos] = (int8_t)code;
-        if ((lane & 31) == 0) a.ps[grow * a.ntb + (pos >> 5)] = exp_to16(es == kExpNaN ? kExpNaN : es - 6);
+      __builtin_amdgcn_sched_barrier(0);  // one slot's K rows in flight at a time (VGPRs)
+    }
+    mx = wave_max_f32(mx);
+    float sum = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      v[s] = pos < a.k_top ? expf(v[s] - mx) : 0.0f;
+      sum += v[s];
+    }
+    sum = wave_sum_f32(sum);
+    // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
+    if (lane < 16) bm[lane] = 0u;
+    for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(rowbuf)[c] = 0u;
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (pos < a.k_top) {
+        v[s] = round_bfloat(v[s] / sum, a.bfloat, kRoundNearest, 1);
+        atomicMax(&bm[ix[s] >> 5], __float_as_uint(v[s]) & 0x7FFFFFFFu);
       }
     }
+    wave_lds_sync();
+    if (lane < a.ntb) {
+      int e_raw;
+      const int es = scale_exponent(bm[lane], 127, &e_raw);
+      const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
+      a.ps[grow * a.ntb + lane] = exp_to16(es == kExpNaN ? kExpNaN : es - 6);
+      bm[lane] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);  // 0: NaN block
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (pos < a.k_top) {
+        const uint32_t e = bm[ix[s] >> 5];
+        int code = 0;
+        if (e & 0xFFFFu) {
+          const int es = (int)(e & 0xFFFFu) - 1024;
+          const float x = (e & 0x10000u) ? v[s] * 0.0f : v[s];
+          code = (int)round_code(x, es, 8, kRoundNearest);
+        }
+        reinterpret_cast<int8_t*>(rowbuf)[ix[s]] = (int8_t)code;
+      }
+    }
+    wave_lds_sync();
+    for (int c = lane; c < a.tpad / 4; c += 64)
+      reinterpret_cast<uint32_t*>(a.pc + grow * a.tpad)[c] = reinterpret_cast<const uint32_t*>(rowbuf)[c];
+    wave_lds_sync();
   }
 }
 
@@ -251,6 +481,25 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(TopkArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + wave;
   if (row >= a.rows) return;  // wave-uniform
+  const TopkLdsV2 sc = carve_topk(smem + (size_t)wave * topk_scratch_bytes(S), S);
+  const float* src = a.vals + row * a.ld;
+  for (int pos = lane; pos < a.n; pos += 64) sc.A[pos] = pack_ki(order_key(src[pos]), (uint32_t)pos);
+  wave_lds_sync();
+  lds_topk<S>(sc, a.n, a.k, lane);
+  for (int pos = lane; pos < a.k; pos += 64) {
+    const uint32_t ix = (uint32_t)sc.A[pos];
+    a.out_idx[row * a.k + pos] = (int64_t)ix;
+    if (a.out_vals) a.out_vals[row * a.k + pos] = src[ix];
+  }
+}
+
+// previous register-resident form (mxa_topk.hpp), kept for A/B timing (MXA_TOPK_V1)
+template <int S>
+__global__ __launch_bounds__(256) void topk_rows_v1_kernel(TopkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= a.rows) return;  // wave-uniform
   TopkLds sc;
   sc.a = reinterpret_cast<uint64_t*>(smem) + (size_t)wave * (2 * 64 * S + kTopkStack / 2);
   sc.b = sc.a + 64 * S;
@@ -274,6 +523,7 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(TopkArgs a) {
     }
   }
 }
+
 
 // ---- mx.matmul: C[b] = MX(A[b], along K) @ MX(B[b], along K) ---------------
 struct MatmulArgs {
@@ -390,7 +640,7 @@ extern "C" int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p) {
 template <int S>
 static int launch_scores(const ScoresArgs& sa, int BH, int N, hipStream_t stream) {
   const size_t lds = (size_t)2 * kRowsPerWG * sa.tpad * sizeof(float) +
-                     (size_t)4 * (2 * 64 * S + kTopkStack / 2) * sizeof(uint64_t);
+                     (size_t)4 * topk_scratch_bytes(S);
   dim3 grid((unsigned)((N + kRowsPerWG - 1) / kRowsPerWG), (unsigned)BH);
   if (lds > 65536 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&scores_topk_kernel<S>),
@@ -398,6 +648,33 @@ static int launch_scores(const ScoresArgs& sa, int BH, int N, hipStream_t stream
     return MXA_ERR_LAUNCH;
   hipLaunchKernelGGL(scores_topk_kernel<S>, grid, dim3(256), lds, stream, sa);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+template <int S, bool MUL, bool TOPK>
+static int launch_rows_s(const RowsArgs& ra, int BH, hipStream_t stream) {
+  const size_t lds = rows_lds_bytes(ra.s.T, ra.kst, ra.s.nbd, S, ra.s.tpad);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows_kernel<S, MUL, TOPK>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const dim3 grid((unsigned)((ra.s.N + ra.rows_per_wg - 1) / ra.rows_per_wg), (unsigned)BH);
+  hipLaunchKernelGGL((attn_rows_kernel<S, MUL, TOPK>), grid, dim3(64 * kRowsWaves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+template <int S>
+static int launch_rows_mode(const RowsArgs& ra, int BH, hipStream_t stream) {
+  if (!ra.s.top_k) return launch_rows_s<S, false, false>(ra, BH, stream);
+  if (ra.s.mul_combine && !ra.key_is_true) return launch_rows_s<S, true, true>(ra, BH, stream);
+  return launch_rows_s<S, false, true>(ra, BH, stream);
+}
+
+static int launch_rows(const RowsArgs& ra, int S, int BH, hipStream_t stream) {
+  switch (S) {
+    case 1: return launch_rows_mode<1>(ra, BH, stream);
+    case 2: return launch_rows_mode<2>(ra, BH, stream);
+    case 4: return launch_rows_mode<4>(ra, BH, stream);
+    default: return launch_rows_mode<8>(ra, BH, stream);
+  }
 }
 
 static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev) {
@@ -422,6 +699,13 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     default: break;
   }
   const bool need_pred = p->top_k && p->approx;
+  // row-oriented fused kernel when the head's key operand fits LDS (attn_rows_kernel)
+  const int S = (p->T + 63) / 64;
+  const int rows_S = S <= 1 ? 1 : (S <= 2 ? 2 : (S <= 4 ? 4 : 8));
+  const int kst = L.dpad + 16;
+  const char* path_env = getenv("MXA_ATTN_PATH");
+  const bool rows_path = L.nbd <= kMaxNB && rows_lds_bytes(p->T, kst, L.nbd, rows_S, L.tpad) <= 160 * 1024 &&
+                         !(path_env && std::string(path_env) == "tiles");
 
   RowsPrepArgs rq{};
   rq.x = p->q; rq.s0 = p->q_strides[0]; rq.s1 = p->q_strides[1]; rq.s2 = p->q_strides[2];
@@ -480,8 +764,14 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   sa.idx_out = p->idx_out; sa.true_out = p->true_out; sa.pred_out = p->pred_out;
   sa.pc = reinterpret_cast<int8_t*>(ws + L.pc);
   sa.ps = reinterpret_cast<int16_t*>(ws + L.ps);
-  const int S = (p->T + 63) / 64;
-  if (S <= 1) rc = launch_scores<1>(sa, (int)BH, p->N, stream);
+  if (rows_path) {
+    RowsArgs ra{};
+    ra.s = sa;
+    ra.kst = kst;
+    ra.key_is_true = !need_pred;
+    ra.rows_per_wg = p->N;
+    rc = launch_rows(ra, rows_S, (int)BH, stream);
+  } else if (S <= 1) rc = launch_scores<1>(sa, (int)BH, p->N, stream);
   else if (S <= 2) rc = launch_scores<2>(sa, (int)BH, p->N, stream);
   else if (S <= 4) rc = launch_scores<4>(sa, (int)BH, p->N, stream);
   else rc = launch_scores<8>(sa, (int)BH, p->N, stream);
@@ -530,8 +820,11 @@ extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream,
 
 template <int S>
 static int launch_topk(const TopkArgs& ta, hipStream_t stream) {
-  const size_t lds = (size_t)4 * (2 * 64 * S + kTopkStack / 2) * sizeof(uint64_t);
-  hipLaunchKernelGGL(topk_rows_kernel<S>, dim3((unsigned)((ta.rows + 3) / 4)), dim3(256), lds, stream, ta);
+  const dim3 grid((unsigned)((ta.rows + 3) / 4));
+  if (getenv("MXA_TOPK_V1"))
+    hipLaunchKernelGGL(topk_rows_v1_kernel<S>, grid, dim3(256), (size_t)4 * (2 * 64 * S + kTopkStack / 2) * 8, stream, ta);
+  else
+    hipLaunchKernelGGL(topk_rows_kernel<S>, grid, dim3(256), (size_t)4 * topk_scratch_bytes(S), stream, ta);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 

@@ -216,10 +216,10 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
                         ((uint32_t)(op[2] & 0xFF) << 16) | ((uint32_t)(op[3] & 0xFF) << 24);
     if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
     if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
-    if (sub == 0) {
-      if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
-      if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
-    }
+  }
+  if (valid && sub == 0) {
+    if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
+    if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
   }
 }
 

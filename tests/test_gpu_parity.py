@@ -239,6 +239,71 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
         assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
 
 
+def _attn_both_paths(M, q, k, v, scale, **kw):
+    """Run the fused op on the row-oriented kernel (default) and on the MFMA
+    score-tile kernel (MXA_ATTN_PATH=tiles)."""
+    res = []
+    for path in (None, "tiles"):
+        if path:
+            os.environ["MXA_ATTN_PATH"] = path
+        try:
+            res.append(M.mx_topk_attention(dev(q), dev(k), dev(v), scale, return_scores=True, **kw))
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("MXA_ATTN_PATH", None)
+    return [[host(t) for t in r] for r in res]
+
+
+def _check_vs_oracle(got, r, what):
+    out, idx, true_s, pred_s = got
+    same(true_s, r["true"], what + " true")
+    same(pred_s, r["pred"], what + " pred")
+    same(idx, r["idx"], what + " idx")
+    nan_o, nan_r = np.isnan(out), np.isnan(r["out"])
+    same(nan_o, nan_r, what + " NaN rows")
+    fin = ~nan_r.any(-1)
+    assert O.normwise_rel_err(out[fin], r["out"][fin]) <= OUT_TOL, what
+
+
+@pytest.mark.parametrize("D", [32, 64, 72, 128])
+@pytest.mark.parametrize("N,T,k", [(197, 197, 20), (256, 256, 154), (5, 64, 7), (1, 20, 5), (70, 130, 65)])
+def test_expred_rows_and_tiles_paths_vs_oracle(M, D, N, T, k):
+    """Both fused kernels against the oracle over head dims of 1..4 MX blocks,
+    short and long rows, k in both top-k branches."""
+    rng = np.random.default_rng(D * 1000 + N)
+    B, H = 2, 3
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    scale = float(D) ** -0.5
+    rows, tiles = _attn_both_paths(M, q, kk, v, scale, k_top=k)
+    r = O.attention(q, kk, v, scale, k_top=k)
+    _check_vs_oracle(rows, r, "rows")
+    _check_vs_oracle(tiles, r, "tiles")
+
+
+def test_expred_special_rows(M):
+    """Zero K rows (exponent -126 blocks), a wide exponent spread, NaN / Inf
+    inputs, rows whose true scores overflow, all-zero query rows."""
+    rng = np.random.default_rng(5)
+    B, H, N, T, D, k = 2, 4, 197, 197, 64, 20
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    kk[0, 0, 7, :] = 0.0                        # zero key row: exponent -126 blocks, head falls back
+    kk[0, 1, 11, 32:] *= np.float32(2.0 ** 40)  # exponent spread > 24 bits
+    q[0, 2, 3, 5] = np.nan                      # NaN row
+    q[0, 2, 9, 40] = np.inf                     # Inf row
+    kk[1, 0, 50, 3] = np.nan                    # NaN key: head's preds all NaN in block 0
+    q[1, 1, 17, :] *= np.float32(2.0 ** 100)    # true scores overflow for this row
+    kk[1, 1, :, :] *= np.float32(2.0 ** 30)
+    q[1, 2, :4, :] = 0.0                        # zero query rows (all preds tie)
+    rows, tiles = _attn_both_paths(M, q, kk, v, 0.125, k_top=k)
+    r = O.attention(q, kk, v, 0.125, k_top=k)
+    _check_vs_oracle(rows, r, "rows")
+    _check_vs_oracle(tiles, r, "tiles")
+
+
 def test_pixart_cross_full_batch(M):
     B, H, N, T, D, k = 8, 16, 256, 120, 72, 20
     rng = np.random.default_rng(0)
