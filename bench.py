@@ -126,6 +126,25 @@ def parity_sample(c, q, k, v, bias, out, idx, heads=4):
             "out_tol": 1e-3}
 
 
+def timed_region(run, world, sync, device):
+    """Barrier + device sync on both sides of `run`, then the MAX of the elapsed
+    wall time over ranks (the only collectives of the benchmark)."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,19 +197,10 @@ def main():
     stage_ms = (ctypes.c_float * 5)()
     stream = torch.cuda.current_stream(device).cuda_stream
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    N.check(N.lib().mxa_attention_timed(ctypes.byref(p), stream, args.steps, stage_ms), "mxa_attention_timed")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(
+        lambda: N.check(N.lib().mxa_attention_timed(ctypes.byref(p), stream, args.steps, stage_ms),
+                        "mxa_attention_timed"),
+        world, torch.cuda.synchronize, device)
 
     tokens = world * c["B"] * c["N"] * args.steps
     value = tokens / elapsed

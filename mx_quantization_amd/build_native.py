@@ -14,42 +14,44 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmxa.so")
 SOURCES = ["mxa_quant.hip", "mxa_attn.hip"]
-HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_topk.hpp", "mxa_topk_lds.hpp", "mxa_exp_lut.h", "../../include/mxa.h"]
+HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_topk.hpp", "mxa_topk_lds.hpp", "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(lib=LIB):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
-        return LIB
+def build(force=False, verbose=True, phase_prof=False):
+    """phase_prof: instrumented build (per-phase cycle counters of the fused
+    kernel, tools/phase_prof.py) into libmxa_prof.so; never the product."""
+    lib = LIB.replace("libmxa.so", "libmxa_prof.so") if phase_prof else LIB
+    if not force and not _stale(lib):
+        return lib
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        obj = os.path.join(CSRC, src.replace(".hip", "_prof.o" if phase_prof else ".o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                "-Wall", "-Wno-unused-function", "-I", os.path.join(HERE, "..", "include"),
-               "-c", os.path.join(CSRC, src), "-o", obj]
+               "-c", os.path.join(CSRC, src), "-o", obj] + (["-DMXA_PHASE_PROF"] if phase_prof else [])
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    print(LIB)
+    print(build(force="--force" in sys.argv, phase_prof="--phase-prof" in sys.argv))

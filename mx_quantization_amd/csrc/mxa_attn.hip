@@ -122,12 +122,8 @@ __device__ void finish_row(const ScoresArgs& a, int64_t grow, float* trow, float
     const int pos = s * 64 + lane;
     if (s * 64 >= a.tpad) break;
     const float x = round_bfloat(pv[s], a.bfloat, kRoundNearest, 1);
-    uint32_t mb = __float_as_uint(x) & 0x7FFFFFFFu;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      const uint32_t w2 = (uint32_t)__shfl_xor((int)mb, o, 32);
-      mb = w2 > mb ? w2 : mb;
-    }
+    const uint32_t mb = half_reduce(__float_as_uint(x) & 0x7FFFFFFFu,
+                                    [](uint32_t u, uint32_t w) { return u > w ? u : w; });
     int e_raw;
     const int es = scale_exponent(mb, 127, &e_raw);
     float xv = x;
@@ -209,193 +205,339 @@ __global__ __launch_bounds__(256) void scores_topk_kernel(ScoresArgs a) {
 }
 
 // ---- row-oriented fused scores + top-k: one wave per query row -------------
-// A workgroup of kRowsWaves waves takes the rows of one head.  The head's key
-// operand (approximator codes for the approximate scores, or the MX codes when
-// the keys are true scores) is staged once in LDS; every wave then computes its
-// row's T scores with v_dot4_i32_i8 per 32-element MX block and an exact fp64
-// block epilogue (the same floats scaled_tile gives), writes them
-// as order keys straight into its LDS top-k array, runs lds_topk, and computes
-// the true scores of the kept keys only.  Softmax, scatter and the MX
-// quantization of P along keys follow; P leaves as MXINT8 codes for pv_kernel.
+// A workgroup of kRowsWaves waves takes the rows of one head.  The head's K
+// tables are staged once in LDS: the MXINT8 codes (true scores) and, for the
+// approximate scores, either the approximator codes (MXINT4 / EXION / partial_*
+// operands, v_dot4 per 32-element block) or, for ex_pred, one sign word per
+// block (pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b)), exact).  Each
+// wave computes its row's T scores with an exact fp64 block epilogue (the floats
+// the reference's fp32 matmul gives), writes them as order keys
+// into its LDS top-k array, runs the exact-order top-k (mxa_topk_lds.hpp), and
+// takes the true scores of the kept keys from the LDS codes.  Softmax, scatter
+// and the MX quantization of P along keys follow; P leaves as MXINT8 codes for
+// pv_kernel.  Each query row arrives in one vector load (lane i holds dword i),
+// prefetched one row ahead.
 constexpr int kRowsWaves = 8;
 constexpr int kMaxNB = 4;  // head dim <= 128
 
-struct RowsArgs {
-  ScoresArgs s;
-  int kst;          // LDS row stride of the key operand table (dpad + 16: conflict-free b128 reads)
-  int key_is_true;  // table holds the K MX codes: the row values are true scores
-  int rows_per_wg;
+#ifdef MXA_PHASE_PROF  // instrumented build only (build_native --phase-prof, tools/phase_prof.py)
+__device__ unsigned long long g_phase_cycles[16];
+// per-wave sums in registers, flushed once per wave (MXA_PHASE_FLUSH)
+#define MXA_PHASE_INIT() \
+  uint64_t ph_t = clock64(); \
+  uint64_t ph_acc[6] = {0, 0, 0, 0, 0, 0}
+#define MXA_PHASE(i)                  \
+  do {                                \
+    const uint64_t ph_n = clock64();  \
+    ph_acc[i] += ph_n - ph_t;         \
+    ph_t = ph_n;                      \
+  } while (0)
+#define MXA_PHASE_FLUSH()                                                   \
+  do {                                                                      \
+    if (lane == 0)                                                          \
+      for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase_cycles[i_], ph_acc[i_]); \
+  } while (0)
+#else
+#define MXA_PHASE_INIT() (void)0
+#define MXA_PHASE(i) (void)0
+#define MXA_PHASE_FLUSH() (void)0
+#endif
+
+enum RowsMode : int {
+  kModeTrue = 0,   // row values are the true scores (approx off, or dense)
+  kModeOpExp = 1,  // approximator codes, block scale 2^(sa + sb)
+  kModeOpMul = 2,  // approximator codes, block scale sa * sb / 4096 (EXION)
+  kModeExSign = 3  // ex_pred: sign words + block exponents
 };
 
-__host__ __device__ inline size_t rows_wave_bytes(int S, int tpad) {
-  return topk_scratch_bytes(S) + (size_t)tpad * 4 + 64;
-}
-__host__ __device__ inline size_t rows_lds_bytes(int T, int kst, int nbd, int S, int tpad) {
-  return (size_t)T * kst + (((size_t)T * nbd * 2 + 15) & ~(size_t)15) + (size_t)kRowsWaves * rows_wave_bytes(S, tpad);
+struct RowsArgs {
+  ScoresArgs s;
+  const uint32_t* qsg;  // [B*H*N][nbd] sign words of the Q codes (ex_pred)
+  const uint32_t* ksg;  // [B*H*T][nbd] sign words of the K codes (ex_pred)
+  int D;
+  int kst;  // LDS row stride of the code tables (dpad + 16: conflict-free b128 reads)
+  int rows_per_wg;
+  int dbg;  // instrumented build only: phases to skip (tools/phase_prof.py), 0 otherwise
+};
+
+#ifdef MXA_PHASE_PROF
+#define MXA_SKIP(bit) (ra.dbg & (bit))
+#else
+#define MXA_SKIP(bit) false
+#endif
+
+__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+struct RowsLds {
+  size_t mx, sT, op, sA, sg, waves, per_wave, total;
+};
+__host__ __device__ inline RowsLds rows_lds(int mode, int T, int kst, int nbd, int S, int tpad, bool topk) {
+  RowsLds L;
+  size_t o = 0;
+  L.mx = o;
+  o += al16((size_t)T * kst);
+  L.sT = o;
+  o += al16((size_t)T * nbd * 2);
+  L.op = o;
+  if (mode == kModeOpExp || mode == kModeOpMul) o += al16((size_t)T * kst);
+  L.sA = o;
+  if (mode != kModeTrue) o += al16((size_t)T * nbd * 2);
+  L.sg = o;
+  if (mode == kModeExSign) o += al16((size_t)T * nbd * 4);
+  L.waves = o;
+  L.per_wave = topk_scratch_bytes(S) + (topk ? al16(tpad) : (size_t)tpad * 4) + 64;
+  L.total = o + kRowsWaves * L.per_wave;
+  return L;
 }
 
-// uniform row of int8 codes (dpad bytes) -> registers, blocks < nbd
-__device__ __forceinline__ void load_row_codes(const int8_t* src, int nbd, uint32_t (&w)[kMaxNB * 8]) {
+// Block-outer dot products of one uniform query row (codes at qrow, code-unit
+// exponents at qs) with up to S LDS key rows per lane (jj[s], where ok[s]):
+// acc[s] = exact sum_b I_b * scale_b in fp64 (EXP scale 2^(sa + sb), MUL scale
+// sa * sb / 4096).  The query block's 8 words come in by scalar loads, so only 8
+// SGPRs are live at a time.
+typedef __attribute__((address_space(4))) const uint32_t* cu32;
+
+__device__ __forceinline__ int s_exp16(const int16_t* base, int64_t i) {
+  const uint32_t d = ((cu32)(base + (i & ~(int64_t)1)))[0];
+  return exp_from16((int16_t)(i & 1 ? d >> 16 : d & 0xFFFFu));
+}
+
+template <int S, bool MUL>
+__device__ __forceinline__ void dot_slots(const int8_t* qrow, const int16_t* qs, int64_t qs0, int nbd, const int8_t* tab, int kst,
+                                          const int16_t* tsc, const int (&jj)[S], const bool (&ok)[S],
+                                          double (&acc)[S], bool (&nan)[S]) {
 #pragma unroll
-  for (int b = 0; b < kMaxNB; ++b) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (b < nbd) v = *reinterpret_cast<const uint4*>(src + 32 * b + 16 * c);
-      // the row is wave-uniform: keep it in SGPRs (v_dot4 takes one scalar operand)
-      w[8 * b + 4 * c] = __builtin_amdgcn_readfirstlane(v.x);
-      w[8 * b + 4 * c + 1] = __builtin_amdgcn_readfirstlane(v.y);
-      w[8 * b + 4 * c + 2] = __builtin_amdgcn_readfirstlane(v.z);
-      w[8 * b + 4 * c + 3] = __builtin_amdgcn_readfirstlane(v.w);
-    }
+  for (int s = 0; s < S; ++s) {
+    acc[s] = 0.0;
+    nan[s] = false;
   }
-}
-
-// fl32(exact sum_b I_b * scale_b): EXP scale 2^(sa + sb), MUL scale sa * sb / 4096
-template <bool MUL>
-__device__ __forceinline__ float block_scaled_dot(const uint32_t (&qw)[kMaxNB * 8], const int (&qs)[kMaxNB],
-                                                  const int8_t* krow, const int16_t* ks, int nbd) {
-  double acc = 0.0;
-  bool nan = false;
 #pragma unroll
   for (int b = 0; b < kMaxNB; ++b) {
     if (b < nbd) {
-      const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
-      const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
-      int I = 0;
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 0], (int)x0.x, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 1], (int)x0.y, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 2], (int)x0.z, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 3], (int)x0.w, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 4], (int)x1.x, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 5], (int)x1.y, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 6], (int)x1.z, I, false);
-      I = __builtin_amdgcn_sdot4((int)qw[8 * b + 7], (int)x1.w, I, false);
-      const int e = exp_from16(ks[b]);
-      if (e == kExpNaN || qs[b] == kExpNaN) nan = true;
-      else if (MUL) acc += (double)I * (double)(qs[b] * e) * (1.0 / 4096.0);
-      else acc += (double)I * pow2d(qs[b] + e);
+      const cu32 src = (cu32)(qrow + 32 * b);
+      uint32_t w[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) w[c] = src[c];
+      const int qe = s_exp16(qs, qs0 + b);  // (absolute index: the dword load needs the array's alignment)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (ok[s]) {
+          const int8_t* kr = tab + (size_t)jj[s] * kst + 32 * b;
+          const uint4 x0 = *reinterpret_cast<const uint4*>(kr);
+          const uint4 x1 = *reinterpret_cast<const uint4*>(kr + 16);
+          int I = 0;
+          I = __builtin_amdgcn_sdot4((int)w[0], (int)x0.x, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[1], (int)x0.y, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[2], (int)x0.z, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[3], (int)x0.w, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[4], (int)x1.x, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[5], (int)x1.y, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[6], (int)x1.z, I, false);
+          I = __builtin_amdgcn_sdot4((int)w[7], (int)x1.w, I, false);
+          const int e = exp_from16(tsc[jj[s] * nbd + b]);
+          if (e == kExpNaN || qe == kExpNaN) nan[s] = true;
+          else if (MUL) acc[s] += (double)I * (double)(qe * e) * (1.0 / 4096.0);
+          else acc[s] += (double)I * pow2d(qe + e);
+        }
+      }
     }
   }
-  return nan ? __uint_as_float(0x7FC00000u) : (float)acc;
 }
 
-template <int S, bool MUL, bool TOPK>
+template <int S, int MODE, bool TOPK>
 __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs ra) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ScoresArgs& a = ra.s;
+  constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.y;
-  const int T = a.T, nbd = a.nbd;
+  const int T = a.T, nbd = a.nbd, kst = ra.kst;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  int8_t* tab = reinterpret_cast<int8_t*>(smem);                         // [T][kst]
-  int16_t* tsc = reinterpret_cast<int16_t*>(smem + (size_t)T * ra.kst);  // [T][nbd]
-  unsigned char* wbase = smem + (size_t)T * ra.kst + (((size_t)T * nbd * 2 + 15) & ~(size_t)15) +
-                         (size_t)wave * rows_wave_bytes(S, a.tpad);
+  const RowsLds L = rows_lds(MODE, T, kst, nbd, S, a.tpad, TOPK);
+  int8_t* tmx = reinterpret_cast<int8_t*>(smem + L.mx);      // [T][kst] K MXINT8 codes
+  int16_t* tsT = reinterpret_cast<int16_t*>(smem + L.sT);    // [T][nbd] their code-unit exponents
+  int8_t* top = reinterpret_cast<int8_t*>(smem + L.op);      // [T][kst] K approximator codes
+  int16_t* tsA = reinterpret_cast<int16_t*>(smem + L.sA);    // [T][nbd] approximator scales
+  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);  // [T][nbd] ex_pred sign words
+  unsigned char* wbase = smem + L.waves + (size_t)wave * L.per_wave;
   const TopkLdsV2 sc = carve_topk(wbase, S);
-  float* rowbuf = reinterpret_cast<float*>(wbase + topk_scratch_bytes(S));  // [tpad]
-  uint32_t* bm = reinterpret_cast<uint32_t*>(rowbuf + a.tpad);               // [16]
+  unsigned char* rowbuf = wbase + topk_scratch_bytes(S);  // P code row (top-k) / score row (dense)
+  uint32_t* bm = reinterpret_cast<uint32_t*>(rowbuf + (TOPK ? al16(a.tpad) : (size_t)a.tpad * 4));
 
-  // ---- stage the head's key operand ----------------------------------------
-  const int8_t* ksrc = (ra.key_is_true ? a.kc : a.kop) + (int64_t)bh * T * a.dpad;
-  const int16_t* ssrc = (ra.key_is_true ? a.ksT : a.ksA) + (int64_t)bh * T * nbd;
+  // ---- stage the head's K tables -------------------------------------------
+  MXA_PHASE_INIT();
+  const int64_t kb = (int64_t)bh * T;
   const int cpr = a.dpad / 16;
   for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
     const int j = i / cpr, c = i - j * cpr;
-    *reinterpret_cast<uint4*>(tab + (size_t)j * ra.kst + 16 * c) =
-        *reinterpret_cast<const uint4*>(ksrc + (int64_t)j * a.dpad + 16 * c);
+    *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
+        *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
+    if (kOp)
+      *reinterpret_cast<uint4*>(top + (size_t)j * kst + 16 * c) =
+          *reinterpret_cast<const uint4*>(a.kop + (kb + j) * a.dpad + 16 * c);
   }
-  for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tsc[i] = ssrc[i];
+  for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
+    tsT[i] = a.ksT[kb * nbd + i];
+    if (MODE != kModeTrue) tsA[i] = a.ksA[kb * nbd + i];
+    if (MODE == kModeExSign) tsg[i] = ra.ksg[kb * nbd + i];
+  }
   __syncthreads();
+  MXA_PHASE(0);
 
-  const int64_t kb = (int64_t)bh * T;
   const int r0 = blockIdx.x * ra.rows_per_wg;
   const int r1 = min(a.N, r0 + ra.rows_per_wg);
-  for (int r = r0 + wave; r < r1; r += kRowsWaves) {
+  for (int r = r0 + __builtin_amdgcn_readfirstlane(wave); r < r1; r += kRowsWaves) {
     const int64_t grow = (int64_t)bh * a.N + r;
     const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
+    const int8_t* qmx = a.qc + grow * a.dpad;
+
     // ---- the row's T values (approximate scores, or true scores) -----------
-    uint32_t qw[kMaxNB * 8];
-    int qs[kMaxNB];
-    load_row_codes((ra.key_is_true ? a.qc : a.qop) + grow * a.dpad, nbd, qw);
+    float vals[S];
+    if (MXA_SKIP(4)) {
 #pragma unroll
-    for (int b = 0; b < kMaxNB; ++b)
-      qs[b] = b < nbd ? exp_from16((ra.key_is_true ? a.qsT : a.qsA)[grow * nbd + b]) : 0;
-#pragma unroll 1
+      for (int s = 0; s < S; ++s) vals[s] = (float)((64 * s + lane) & 7);
+    } else if constexpr (MODE == kModeExSign) {
+      // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
+      uint32_t sq[kMaxNB];
+      int eq[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) {
+        sq[b] = b < nbd ? ((cu32)(ra.qsg + grow * nbd))[b] : 0u;
+        eq[b] = b < nbd ? s_exp16(a.qsA, grow * nbd + b) : 0;
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = 64 * s + lane;
+        double acc = 0.0;
+        bool nan = false;
+        if (j < T) {
+#pragma unroll
+          for (int b = 0; b < kMaxNB; ++b) {
+            if (b < nbd) {
+              const int e = exp_from16(tsA[j * nbd + b]);
+              if (e == kExpNaN || eq[b] == kExpNaN) nan = true;
+              const int m = min(32, ra.D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
+              acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
+            }
+          }
+        }
+        vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+      }
+    } else {
+      int jj[S];
+      bool ok[S];
+      double acc[S];
+      bool nan[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        jj[s] = min(64 * s + lane, T - 1);
+        ok[s] = 64 * s + lane < T;
+      }
+      if (MODE == kModeTrue) dot_slots<S, false>(qmx, a.qsT, grow * nbd, nbd, tmx, kst, tsT, jj, ok, acc, nan);
+      else dot_slots<S, MODE == kModeOpMul>(a.qop + grow * a.dpad, a.qsA, grow * nbd, nbd, top, kst, tsA, jj, ok,
+                                            acc, nan);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        vals[s] = nan[s] ? __uint_as_float(0x7FC00000u) : (float)acc[s];
+        // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)   (matmul.py:88-91, caller)
+        if (MODE == kModeTrue) vals[s] = round_bfloat(vals[s], a.bfloat, kRoundNearest, 1) * a.scale;
+      }
+    }
+#pragma unroll
     for (int s = 0; s < S; ++s) {
       const int j = 64 * s + lane;
       if (j < T) {
-        float v = block_scaled_dot<MUL>(qw, qs, tab + (size_t)j * ra.kst, tsc + (size_t)j * nbd, nbd);
-        const float bv = brow ? brow[(int64_t)j * a.bs3] : 0.0f;
-        if (ra.key_is_true) {
-          // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)   (matmul.py:88-91, caller)
-          v = round_bfloat(v, a.bfloat, kRoundNearest, 1) * a.scale;
-          if (brow) v = v + bv;
+        float v = vals[s];
+        if (brow) v = v + brow[(int64_t)j * a.bs3];
+        if (MODE == kModeTrue) {
           if (a.true_out) a.true_out[grow * T + j] = v;
-        } else {
-          if (brow) v = v + bv;
-          if (a.pred_out) a.pred_out[grow * T + j] = v;
+        } else if (a.pred_out) {
+          a.pred_out[grow * T + j] = v;
         }
         if (TOPK) sc.A[j] = pack_ki(order_key(v), (uint32_t)j);
-        else rowbuf[j] = v;
+        else reinterpret_cast<float*>(rowbuf)[j] = v;
       }
     }
+    if (TOPK) {  // clear the P row and the block maxima off the critical path
+      if (lane < 16) bm[lane] = 0u;
+      for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(rowbuf)[c] = 0u;
+    }
     wave_lds_sync();
+    MXA_PHASE(1);
 
     if constexpr (!TOPK) {  // dense: softmax over every key (finish_row's dense branch)
-      finish_row<S>(a, grow, rowbuf, rowbuf, sc, lane);
+      finish_row<S>(a, grow, reinterpret_cast<float*>(rowbuf), reinterpret_cast<float*>(rowbuf), sc, lane);
       wave_lds_sync();
       continue;
     }
-    lds_topk<S>(sc, T, a.k_top, lane);
+    const bool done = MXA_SKIP(1) ? true : lds_select<S>(sc, T, a.k_top, lane);
+    MXA_PHASE(2);
+    if (!done) lds_sort_prefix<S>(sc, a.k_top - 1, lane);
+    MXA_PHASE(3);
+
     // ---- vals = true.gather(idx); softmax(vals) ------------------------------
-    // true scores of the kept keys only (and of every key for the debug output)
-    uint32_t tw[kMaxNB * 8];
-    int ts[kMaxNB];
-    load_row_codes(a.qc + grow * a.dpad, nbd, tw);
+    auto true_scores = [&](const int (&jj)[S], const bool (&ok)[S], float (&t)[S]) {
+      double acc[S];
+      bool nan[S];
+      dot_slots<S, false>(qmx, a.qsT, grow * nbd, nbd, tmx, kst, tsT, jj, ok, acc, nan);
 #pragma unroll
-    for (int b = 0; b < kMaxNB; ++b) ts[b] = b < nbd ? exp_from16(a.qsT[grow * nbd + b]) : 0;
-    auto true_score = [&](int j) {
-      float t = block_scaled_dot<false>(tw, ts, a.kc + (kb + j) * a.dpad, a.ksT + (kb + j) * nbd, nbd);
-      t = round_bfloat(t, a.bfloat, kRoundNearest, 1) * a.scale;
-      if (brow) t = t + brow[(int64_t)j * a.bs3];
-      return t;
+      for (int s = 0; s < S; ++s) {
+        t[s] = nan[s] ? __uint_as_float(0x7FC00000u) : (float)acc[s];
+        t[s] = round_bfloat(t[s], a.bfloat, kRoundNearest, 1) * a.scale;
+        if (brow && ok[s]) t[s] = t[s] + brow[(int64_t)jj[s] * a.bs3];
+      }
     };
-    if (a.true_out && !ra.key_is_true)
-      for (int j = lane; j < T; j += 64) a.true_out[grow * T + j] = true_score(j);
+    if (a.true_out && MODE != kModeTrue) {  // debug output: every key's true score
+      int jj[S];
+      bool ok[S];
+      float t[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        jj[s] = min(64 * s + lane, T - 1);
+        ok[s] = 64 * s + lane < T;
+      }
+      true_scores(jj, ok, t);
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (ok[s]) a.true_out[grow * T + jj[s]] = t[s];
+    }
+    int ix[S];
+    bool kept[S];
     float v[S];
-    uint32_t ix[S];
-    float mx = -INFINITY;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int pos = 64 * s + lane;
-      v[s] = -INFINITY;
-      ix[s] = 0u;
-      if (pos < a.k_top) {
-        ix[s] = (uint32_t)sc.A[pos];
-        if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
-        v[s] = true_score((int)ix[s]);
-        mx = fmaxf(mx, v[s]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one slot's K rows in flight at a time (VGPRs)
+      kept[s] = pos < a.k_top;
+      ix[s] = kept[s] ? (int)(uint32_t)sc.A[pos] : 0;
+      if (kept[s] && a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
     }
+    if (MXA_SKIP(8)) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) v[s] = (float)(ix[s] & 3);
+    } else {
+      true_scores(ix, kept, v);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < S; ++s) mx = kept[s] ? fmaxf(mx, v[s]) : mx;
     mx = wave_max_f32(mx);
     float sum = 0.0f;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pos = 64 * s + lane;
-      v[s] = pos < a.k_top ? expf(v[s] - mx) : 0.0f;
+      v[s] = kept[s] ? expf(v[s] - mx) : 0.0f;
       sum += v[s];
     }
     sum = wave_sum_f32(sum);
+    MXA_PHASE(4);
+
     // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
-    if (lane < 16) bm[lane] = 0u;
-    for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(rowbuf)[c] = 0u;
-    wave_lds_sync();
+    if (MXA_SKIP(2)) {
+      wave_lds_sync();
+      continue;
+    }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pos = 64 * s + lane;
-      if (pos < a.k_top) {
+      if (kept[s]) {
         v[s] = round_bfloat(v[s] / sum, a.bfloat, kRoundNearest, 1);
         atomicMax(&bm[ix[s] >> 5], __float_as_uint(v[s]) & 0x7FFFFFFFu);
       }
@@ -411,8 +553,7 @@ __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs 
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const int pos = 64 * s + lane;
-      if (pos < a.k_top) {
+      if (kept[s]) {
         const uint32_t e = bm[ix[s] >> 5];
         int code = 0;
         if (e & 0xFFFFu) {
@@ -427,7 +568,9 @@ __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs 
     for (int c = lane; c < a.tpad / 4; c += 64)
       reinterpret_cast<uint32_t*>(a.pc + grow * a.tpad)[c] = reinterpret_cast<const uint32_t*>(rowbuf)[c];
     wave_lds_sync();
+    MXA_PHASE(5);
   }
+  MXA_PHASE_FLUSH();
 }
 
 struct PVArgs {
@@ -582,7 +725,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qsT, qsA, kc, kop, ksT, ksA, vt, vs, pc, ps, total;
+  int64_t qc, qop, qsT, qsA, qsg, kc, kop, ksT, ksA, ksg, vt, vs, pc, ps, total;
 };
 
 AttnLayout attn_layout(const mxa_attn_params* p) {
@@ -603,10 +746,12 @@ AttnLayout attn_layout(const mxa_attn_params* p) {
   L.qop = take(qrows * L.dpad);
   L.qsT = take(qrows * L.nbd * 2);
   L.qsA = take(qrows * L.nbd * 2);
+  L.qsg = take(qrows * L.nbd * 4);
   L.kc = take(krows * L.dpad);
   L.kop = take(krows * L.dpad);
   L.ksT = take(krows * L.nbd * 2);
   L.ksA = take(krows * L.nbd * 2);
+  L.ksg = take(krows * L.nbd * 4);
   L.vt = take(BH * p->D * (int64_t)L.tpad);
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
   L.pc = take(qrows * L.tpad);
@@ -620,6 +765,19 @@ bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u
 }  // namespace
 
 extern "C" int mxa_abi_version(void) { return MXA_ABI_VERSION; }
+
+#ifdef MXA_PHASE_PROF
+// instrumented build only: per-phase cycle sums of attn_rows_kernel (lane 0 of each wave)
+extern "C" int mxa_debug_phase_cycles(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 16) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)) != hipSuccess) return MXA_ERR_LAUNCH;
+  }
+  return MXA_OK;
+}
+#endif
 
 extern "C" const char* mxa_status_string(int status) {
   switch (status) {
@@ -650,30 +808,34 @@ static int launch_scores(const ScoresArgs& sa, int BH, int N, hipStream_t stream
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
-template <int S, bool MUL, bool TOPK>
+template <int S, int MODE, bool TOPK>
 static int launch_rows_s(const RowsArgs& ra, int BH, hipStream_t stream) {
-  const size_t lds = rows_lds_bytes(ra.s.T, ra.kst, ra.s.nbd, S, ra.s.tpad);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows_kernel<S, MUL, TOPK>),
+  const size_t lds = rows_lds(MODE, ra.s.T, ra.kst, ra.s.nbd, S, ra.s.tpad, TOPK).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows_kernel<S, MODE, TOPK>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const dim3 grid((unsigned)((ra.s.N + ra.rows_per_wg - 1) / ra.rows_per_wg), (unsigned)BH);
-  hipLaunchKernelGGL((attn_rows_kernel<S, MUL, TOPK>), grid, dim3(64 * kRowsWaves), lds, stream, ra);
+  hipLaunchKernelGGL((attn_rows_kernel<S, MODE, TOPK>), grid, dim3(64 * kRowsWaves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
 template <int S>
-static int launch_rows_mode(const RowsArgs& ra, int BH, hipStream_t stream) {
-  if (!ra.s.top_k) return launch_rows_s<S, false, false>(ra, BH, stream);
-  if (ra.s.mul_combine && !ra.key_is_true) return launch_rows_s<S, true, true>(ra, BH, stream);
-  return launch_rows_s<S, false, true>(ra, BH, stream);
+static int launch_rows_mode(const RowsArgs& ra, int mode, int BH, hipStream_t stream) {
+  if (!ra.s.top_k) return launch_rows_s<S, kModeTrue, false>(ra, BH, stream);
+  switch (mode) {
+    case kModeOpExp: return launch_rows_s<S, kModeOpExp, true>(ra, BH, stream);
+    case kModeOpMul: return launch_rows_s<S, kModeOpMul, true>(ra, BH, stream);
+    case kModeExSign: return launch_rows_s<S, kModeExSign, true>(ra, BH, stream);
+    default: return launch_rows_s<S, kModeTrue, true>(ra, BH, stream);
+  }
 }
 
-static int launch_rows(const RowsArgs& ra, int S, int BH, hipStream_t stream) {
+static int launch_rows(const RowsArgs& ra, int mode, int S, int BH, hipStream_t stream) {
   switch (S) {
-    case 1: return launch_rows_mode<1>(ra, BH, stream);
-    case 2: return launch_rows_mode<2>(ra, BH, stream);
-    case 4: return launch_rows_mode<4>(ra, BH, stream);
-    default: return launch_rows_mode<8>(ra, BH, stream);
+    case 1: return launch_rows_mode<1>(ra, mode, BH, stream);
+    case 2: return launch_rows_mode<2>(ra, mode, BH, stream);
+    case 4: return launch_rows_mode<4>(ra, mode, BH, stream);
+    default: return launch_rows_mode<8>(ra, mode, BH, stream);
   }
 }
 
@@ -699,13 +861,20 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     default: break;
   }
   const bool need_pred = p->top_k && p->approx;
-  // row-oriented fused kernel when the head's key operand fits LDS (attn_rows_kernel)
+  // row-oriented fused kernel when the head's K tables fit LDS (attn_rows_kernel)
   const int S = (p->T + 63) / 64;
   const int rows_S = S <= 1 ? 1 : (S <= 2 ? 2 : (S <= 4 ? 4 : 8));
   const int kst = L.dpad + 16;
+  const int rows_mode = !need_pred ? kModeTrue
+                        : p->pred_mode == MXA_PRED_EX_PRED ? kModeExSign
+                        : p->pred_mode == MXA_PRED_EXION   ? kModeOpMul
+                                                           : kModeOpExp;
   const char* path_env = getenv("MXA_ATTN_PATH");
-  const bool rows_path = L.nbd <= kMaxNB && rows_lds_bytes(p->T, kst, L.nbd, rows_S, L.tpad) <= 160 * 1024 &&
+  const bool rows_path = L.nbd <= kMaxNB &&
+                         rows_lds(rows_mode, p->T, kst, L.nbd, rows_S, L.tpad, p->top_k != 0).total <= 160 * 1024 &&
                          !(path_env && std::string(path_env) == "tiles");
+  // the ex_pred rows kernel derives the sign operand from the MX codes
+  const bool need_op = need_pred && !(rows_path && rows_mode == kModeExSign);
 
   RowsPrepArgs rq{};
   rq.x = p->q; rq.s0 = p->q_strides[0]; rq.s1 = p->q_strides[1]; rq.s2 = p->q_strides[2];
@@ -714,7 +883,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   rq.op_kind = opq; rq.flush = p->flush_subnormals; rq.bfloat = p->bfloat;
   rq.codes = reinterpret_cast<int8_t*>(ws + L.qc);
   rq.sT = reinterpret_cast<int16_t*>(ws + L.qsT);
-  rq.op = need_pred ? reinterpret_cast<int8_t*>(ws + L.qop) : nullptr;
+  rq.op = need_op ? reinterpret_cast<int8_t*>(ws + L.qop) : nullptr;
+  rq.signs = rows_path && rows_mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.qsg) : nullptr;
   rq.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
   if (ev) (void)hipEventRecord(ev[0], stream);
   int rc = launch_rows_prep(rq, stream);
@@ -728,7 +898,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   rk.op_kind = opk;
   rk.codes = reinterpret_cast<int8_t*>(ws + L.kc);
   rk.sT = reinterpret_cast<int16_t*>(ws + L.ksT);
-  rk.op = need_pred ? reinterpret_cast<int8_t*>(ws + L.kop) : nullptr;
+  rk.op = need_op ? reinterpret_cast<int8_t*>(ws + L.kop) : nullptr;
+  rk.signs = rows_path && rows_mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.ksg) : nullptr;
   rk.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.ksA) : nullptr;
   rc = launch_rows_prep(rk, stream);
   if (rc) return rc;
@@ -767,10 +938,15 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   if (rows_path) {
     RowsArgs ra{};
     ra.s = sa;
+    ra.qsg = reinterpret_cast<const uint32_t*>(ws + L.qsg);
+    ra.ksg = reinterpret_cast<const uint32_t*>(ws + L.ksg);
+    ra.D = p->D;
     ra.kst = kst;
-    ra.key_is_true = !need_pred;
     ra.rows_per_wg = p->N;
-    rc = launch_rows(ra, rows_S, (int)BH, stream);
+#ifdef MXA_PHASE_PROF
+    ra.dbg = getenv("MXA_DBG_SKIP") ? atoi(getenv("MXA_DBG_SKIP")) : 0;
+#endif
+    rc = launch_rows(ra, rows_mode, rows_S, (int)BH, stream);
   } else if (S <= 1) rc = launch_scores<1>(sa, (int)BH, p->N, stream);
   else if (S <= 2) rc = launch_scores<2>(sa, (int)BH, p->N, stream);
   else if (S <= 4) rc = launch_scores<4>(sa, (int)BH, p->N, stream);

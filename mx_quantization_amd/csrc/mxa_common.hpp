@@ -10,7 +10,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "mxa_exp_lut.h"
 
 namespace mxa {
 
@@ -21,18 +20,27 @@ constexpr int16_t kExpNaN16 = INT16_MIN;
 
 enum Round : int { kRoundNearest = 0, kRoundFloor = 1, kRoundEven = 2 };  // formats.py:12-16
 
-static __constant__ int32_t c_th_norm[256] = MXA_TH_NORM_INIT;
-static __constant__ int32_t c_th_sub[23] = MXA_TH_SUB_INIT;
-
 // floor(torch.log2(m + 2^-126 * (m == 0))) for m = |x| given as float bits with
 // the sign cleared (mx_ops.py:83-87).  Exact for every float32.
+// fl32(log2 m) rounds up to the next integer for mantissas within `gap` ulps
+// below 2^23; gap depends only on the octave of the exponent.  The closed form
+// below reproduces the per-binade thresholds that tools/gen_exp_lut.py bisects
+// out of torch.log2 (tests/golden/exp_lut.npz; tests/test_oracle_golden.py checks
+// the two agree), and needs no memory access.
 __device__ __forceinline__ int floor_log2_abs_bits(uint32_t ub) {
   if (ub >= 0x7F800000u) return kExpNaN;  // Inf / NaN -> NaN exponent (log2(inf)=inf > emax)
   if (ub == 0u) return -126;
   const uint32_t E = ub >> 23, M = ub & 0x7FFFFFu;
-  if (E) return (int)E - 127 + (M >= (uint32_t)c_th_norm[E] ? 1 : 0);
-  const int j = 31 - __clz((int)M);
-  return -149 + j + (M >= (uint32_t)c_th_sub[j] ? 1 : 0);
+  if (E) {
+    const int e = (int)E - 127;
+    const uint32_t u = (uint32_t)(e >= 0 ? e : -e - 1);
+    const int o = u >= 2u ? 31 - __clz((int)u) : 0;  // octave, 0..6
+    const uint32_t gap = (uint32_t)(0x2C160B05020100ull >> (8 * o)) & 0xFFu;  // 0,1,2,5,11,22,44
+    return e + (M + gap >= (1u << 23) ? 1 : 0);
+  }
+  const int j = 31 - __clz((int)M);  // subnormal: leading mantissa bit
+  const uint32_t gap = j < 17 ? 0u : (uint32_t)(0x160B0B050201ull >> (8 * (j - 17))) & 0xFFu;  // 1,2,5,11,11,22
+  return -149 + j + (j >= 17 && M + gap >= (2u << j) ? 1 : 0);
 }
 
 // Same rule without the zero trick: floor(log2(m)) of a strictly positive finite m.
@@ -121,25 +129,58 @@ __device__ __forceinline__ int mbcnt(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
-    v = w > v ? w : v;
-  }
+// Cross-lane reductions on DPP (no LDS traffic): reduce within each row of 16
+// lanes (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror),
+// then combine the four rows through readlane.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+// reduction over each group of 8 consecutive lanes
+template <class Op>
+__device__ __forceinline__ uint32_t oct_reduce(uint32_t v, Op op) {
+  v = op(v, dpp_u32<0xB1>(v));
+  v = op(v, dpp_u32<0x4E>(v));
+  return op(v, dpp_u32<0x141>(v));
+}
+template <class Op>
+__device__ __forceinline__ uint32_t row16_reduce(uint32_t v, Op op) {
+  v = op(v, dpp_u32<0xB1>(v));
+  v = op(v, dpp_u32<0x4E>(v));
+  v = op(v, dpp_u32<0x141>(v));
+  v = op(v, dpp_u32<0x140>(v));
   return v;
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, Op op) {
+  v = row16_reduce(v, op);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return op(op(r0, r1), op(r2, r3));
+}
+// reduction over each half-wave of 32 lanes (an MX block of 32 positions per slot)
+template <class Op>
+__device__ __forceinline__ uint32_t half_reduce(uint32_t v, Op op) {
+  v = row16_reduce(v, op);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return lane_id() < 32 ? op(r0, r1) : op(r2, r3);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
 }
 
 __device__ __forceinline__ float wave_max_f32(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  return __uint_as_float(wave_reduce(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
+  }));
 }
 
 __device__ __forceinline__ float wave_sum_f32(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  return __uint_as_float(wave_reduce(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
+  }));
 }
 
 // LDS ordering between the lanes of one wave (no workgroup barrier needed).

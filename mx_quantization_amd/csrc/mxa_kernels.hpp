@@ -43,6 +43,7 @@ struct RowsPrepArgs {
   int16_t* sT;    // [rows][nb] exponent of a code unit: es - 6 (nullable)
   int8_t* op;     // [rows][dpad] approximator operand (nullable)
   int16_t* sA;    // [rows][nb] approximator scale (nullable)
+  uint32_t* signs;  // [rows][nb] bit i = (MX code i < 0) (nullable)
 };
 
 // matrices (R x C) at x + b*s0 + h*s1 + r*s2 + c quantized along R in 32-blocks

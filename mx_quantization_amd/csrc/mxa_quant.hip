@@ -151,11 +151,7 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
     const uint32_t ub = __float_as_uint(xv[j]) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;
   }
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const uint32_t w = (uint32_t)__shfl_xor((int)mb, o, 8);
-    mb = w > mb ? w : mb;
-  }
+  mb = oct_reduce(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   int e_raw;
   const int es = scale_exponent(mb, 127, &e_raw);
   const bool nanblk = es == kExpNaN;
@@ -171,11 +167,7 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
     const int ac = code[j] < 0 ? -code[j] : code[j];
     maxc = ac > maxc ? ac : maxc;
   }
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const int w = __shfl_xor(maxc, o, 8);
-    maxc = w > maxc ? w : maxc;
-  }
+  maxc = (int)oct_reduce((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
   // floor(log2(max |MX|)), unclamped; MX max = maxc * 2^(es-6) exactly.
   int eA;
@@ -217,9 +209,16 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
     if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
     if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
   }
+  // packed sign word of the block, bit (4*sub + j) = (code < 0): the exp-sign
+  // operand of ex_pred (codes beyond D are 0, i.e. positive)
+  uint32_t sw = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sw |= (code[j] < 0 ? 1u : 0u) << (4 * sub + j);
+  sw = oct_reduce(sw, [](uint32_t u, uint32_t w) { return u | w; });
   if (valid && sub == 0) {
     if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
     if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
+    if (a.signs) a.signs[row * a.nb + blk] = sw;
   }
 }
 

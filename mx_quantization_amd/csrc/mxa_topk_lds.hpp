@@ -183,59 +183,61 @@ __device__ void lds_segment_sort(const TopkLdsV2& sc, int m, int maxlen, int lan
   wave_lds_sync();
 }
 
-// Full top-k of the row in sc.A[0, n).  On return positions [0, k) hold torch's order.
+// std::nth_element(begin, begin+k-1, end) -- or, when k*64 <= n, the whole
+// std::partial_sort(begin, begin+k, end).  Returns true when [0, k) is final.
 template <int S>
-__device__ void lds_topk(const TopkLdsV2& sc, int n, int k, int lane) {
+__device__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
   uint64_t* A = sc.A;
-  if (k <= 0) return;
+  if (k <= 0) return true;
   if (k * 64 <= n) {  // std::partial_sort(begin, begin+k, end)
     if (lane == 0) {
       s_heap_select(A, 0, k, n);
       s_sort_heap(A, 0, k);
     }
     wave_lds_sync();
-    return;
+    return true;
   }
-  // ---- std::nth_element(begin, begin+k-1, end): __introselect ----------------
-  {
-    int first = 0, last = n;
-    const int nth = k - 1;
-    int depth = 2 * ilog2(n);
-    bool fell_back = false;
-    while (last - first > 3) {
-      if (depth == 0) {
-        if (lane == 0) {
-          s_heap_select(A, first, nth + 1, last);
-          const uint64_t t = A[first];
-          A[first] = A[nth];
-          A[nth] = t;
-        }
-        wave_lds_sync();
-        fell_back = true;
-        break;
-      }
-      --depth;
-      const int cut = lds_partition_any<S>(sc, first, last, lane);
-      if (cut <= nth) first = cut;
-      else last = cut;
-    }
-    if (!fell_back && last - first > 1) {  // __insertion_sort(first, last): <= 3 elements, stable
+  // __introselect
+  int first = 0, last = n;
+  const int nth = k - 1;
+  int depth = 2 * ilog2(n);
+  while (last - first > 3) {
+    if (depth == 0) {
       if (lane == 0) {
-        for (int i = first + 1; i < last; ++i) {
-          const uint64_t x = A[i];
-          int j = i;
-          while (j > first && key_of(x) > key_of(A[j - 1])) {
-            A[j] = A[j - 1];
-            --j;
-          }
-          A[j] = x;
-        }
+        s_heap_select(A, first, nth + 1, last);
+        const uint64_t t = A[first];
+        A[first] = A[nth];
+        A[nth] = t;
       }
       wave_lds_sync();
+      return false;
     }
+    --depth;
+    const int cut = lds_partition_any<S>(sc, first, last, lane);
+    if (cut <= nth) first = cut;
+    else last = cut;
   }
-  // ---- std::sort(begin, begin+k-1): __introsort_loop + final insertion sort --
-  const int m = k - 1;
+  if (last - first > 1) {  // __insertion_sort(first, last): <= 3 elements, stable
+    if (lane == 0) {
+      for (int i = first + 1; i < last; ++i) {
+        const uint64_t x = A[i];
+        int j = i;
+        while (j > first && key_of(x) > key_of(A[j - 1])) {
+          A[j] = A[j - 1];
+          --j;
+        }
+        A[j] = x;
+      }
+    }
+    wave_lds_sync();
+  }
+  return false;
+}
+
+// std::sort(begin, begin+m): __introsort_loop + __final_insertion_sort
+template <int S>
+__device__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
+  uint64_t* A = sc.A;
   if (m <= 1) return;
   // every position starts in its own (trivial) segment
   for (int pos = lane; pos < m; pos += 64) sc.seg[pos] = (uint32_t)pos | ((uint32_t)(pos + 1) << 16);
@@ -270,6 +272,13 @@ __device__ void lds_topk(const TopkLdsV2& sc, int n, int k, int lane) {
   }
   wave_lds_sync();
   lds_segment_sort<S>(sc, m, 16, lane);
+}
+
+// Full top-k of the row in sc.A[0, n) (TopKImpl.h:45-86).  On return positions
+// [0, k) hold torch's order.
+template <int S>
+__device__ void lds_topk(const TopkLdsV2& sc, int n, int k, int lane) {
+  if (!lds_select<S>(sc, n, k, lane)) lds_sort_prefix<S>(sc, k - 1, lane);
 }
 
 }  // namespace mxa

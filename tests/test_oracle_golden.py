@@ -54,6 +54,22 @@ def test_exp_lut_matches_floor_log2():
     assert np.array_equal(want, got)
 
 
+def test_device_closed_form_thresholds_match_lut():
+    """The kernels' closed form (mxa_common.hpp floor_log2_abs_bits: the gap below
+    2^23 by exponent octave) equals the bisected threshold table, entry by entry."""
+    lut = load("exp_lut.npz")
+    for E in range(1, 255):
+        e = E - 127
+        u = e if e >= 0 else -e - 1
+        o = u.bit_length() - 1 if u >= 2 else 0
+        gap = (0x2C160B05020100 >> (8 * o)) & 0xFF
+        assert int(lut["th_norm"][E]) == (1 << 23) - gap, E
+    for j in range(23):
+        gap = 0 if j < 17 else (0x160B0B050201 >> (8 * (j - 17))) & 0xFF
+        th = (2 << j) - gap
+        assert int(lut["th_sub"][j]) == th, j
+
+
 def test_exp_rule_vs_torch_sample():
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(2)

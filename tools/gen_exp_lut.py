@@ -9,8 +9,7 @@ for the top few ulps just below 2^(E+1) the float32-rounded log2 equals E+1,
 so the floor is E+1.  The rule that reproduces torch on every
 positive float32 is  floor(fl32(log2((double) m))).
 
-This script turns that rule into a table the HIP kernels can evaluate with
-two integer ops:
+This script turns that rule into a threshold table:
 
   * normal m (biased exponent field E in 1..254, mantissa M):
         e = E - 127 + (M >= TH_NORM[E])          (TH_NORM[E] == 2^23: never bumps)
@@ -22,7 +21,10 @@ EXHAUSTIVELY over every positive finite float32 against numpy's float64 log2
 (the restatement of torch's float32 log2).  With --torch the
 exhaustive check is repeated against torch.log2 itself.
 
-Output: mx_quantization_amd/csrc/mx_exp_lut.h and tests/golden/exp_lut.npz.
+Output: tests/golden/exp_lut.npz.  The HIP kernels evaluate the same thresholds
+in closed form (the distance below 2^23 depends only on the exponent's octave,
+mxa_common.hpp floor_log2_abs_bits); tests/test_oracle_golden.py checks that
+closed form against this table.
 """
 import argparse
 import os
@@ -96,23 +98,6 @@ def exhaustive_check(th_norm, th_sub, use_torch=False, chunk=1 << 25):
     return bad
 
 
-def write_header(th_norm, th_sub, path):
-    norm = ",\\\n  ".join(", ".join(str(int(v)) for v in th_norm[i:i + 8]) for i in range(0, 256, 8))
-    sub = ", ".join(str(int(v)) for v in th_sub)
-    text = f"""// GENERATED by tools/gen_exp_lut.py -- do not edit.
-// Shared-exponent rule floor(fl32(log2(m))) of mx_ops.py:83-87 (SURVEY.md F5),
-// checked exhaustively over all positive finite float32 against torch.log2.
-//   normal m, biased exponent field E:    e = E - 127 + (mantissa >= TH_NORM[E])
-//   subnormal m, j = floor(log2(mantissa)): e = -149 + j + (mantissa >= TH_SUB[j])
-#pragma once
-#define MXA_TH_NORM_INIT {{\\
-  {norm}}}
-#define MXA_TH_SUB_INIT {{{sub}}}
-"""
-    with open(path, "w") as f:
-        f.write(text)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check", action="store_true", help="exhaustive check vs float64 rule")
@@ -121,7 +106,6 @@ def main():
     th_norm, th_sub = build_tables()
     bumped = int(np.sum((1 << 23) - np.minimum(th_norm[1:255], 1 << 23)))
     print(f"binades with a bump: {int(np.sum(th_norm[1:255] < (1 << 23)))}, bumped floats: {bumped}")
-    write_header(th_norm, th_sub, os.path.join(ROOT, "mx_quantization_amd", "csrc", "mxa_exp_lut.h"))
     np.savez_compressed(os.path.join(ROOT, "tests", "golden", "exp_lut.npz"),
                         th_norm=th_norm.astype(np.int32), th_sub=th_sub.astype(np.int32))
     if args.check:
