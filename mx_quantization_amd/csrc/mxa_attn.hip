@@ -45,7 +45,7 @@ struct ScoresArgs {
 // trow / prow: the row's true and approximate scores in LDS (tpad floats each);
 // prow is reused for the dense P row.
 template <int S>
-__device__ void finish_row(const ScoresArgs& a, int64_t grow, float* trow, float* prow, const TopkLdsV2& sc,
+__device__ __forceinline__ void finish_row(const ScoresArgs& a, int64_t grow, float* trow, float* prow, const TopkLdsV2& sc,
                            int lane) {
   float pv[S];
   if (a.top_k) {
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs 
     }
     const bool done = MXA_SKIP(1) ? true : lds_select<S>(sc, T, a.k_top, lane);
     MXA_PHASE(2);
-    if (!done) lds_sort_prefix<S>(sc, a.k_top - 1, lane);
+    if (!done && !MXA_SKIP(16)) lds_sort_head<S>(sc, a.k_top - 1, lane, MXA_SKIP(32) ? 32 : 0);
     MXA_PHASE(3);
 
     // ---- vals = true.gather(idx); softmax(vals) ------------------------------

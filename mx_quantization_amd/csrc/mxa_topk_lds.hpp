@@ -43,7 +43,7 @@ __device__ __forceinline__ uint32_t key_of(uint64_t v) { return (uint32_t)(v >> 
 
 // __unguarded_partition_pivot(first, last) with cmp = greater; returns the cut.
 template <int S>
-__device__ int lds_partition(const TopkLdsV2& sc, int first, int last, int lane) {
+__device__ __forceinline__ int lds_partition(const TopkLdsV2& sc, int first, int last, int lane) {
   uint64_t* A = sc.A;
   const int len = last - first;
   const int mid = first + len / 2;
@@ -149,9 +149,11 @@ __device__ __forceinline__ int lds_partition_any(const TopkLdsV2& sc, int first,
 }
 
 // Stable sort (key descending) of positions [0, m) within the segments recorded in
-// sc.seg (lo | hi << 16 per position): rank inside the segment by a scan of <= maxlen.
+// sc.seg (lo | hi << 16 per position, segments of <= 16): rank inside the segment
+// by a fully unrolled scan (all 16 key reads in flight).
 template <int S>
-__device__ void lds_segment_sort(const TopkLdsV2& sc, int m, int maxlen, int lane) {
+__device__ __forceinline__ void lds_segment_sort(const TopkLdsV2& sc, int m, int lane) {
+  const uint32_t* keys = reinterpret_cast<const uint32_t*>(sc.A);  // key of position q at [2q + 1]
   uint64_t v[S];
   int dst[S];
 #pragma unroll
@@ -166,11 +168,11 @@ __device__ void lds_segment_sort(const TopkLdsV2& sc, int m, int maxlen, int lan
       if (hi > lo + 1) {
         const uint32_t k = key_of(v[s]);
         int r = 0;
-        for (int j = 0; j < maxlen; ++j) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
           const int q = lo + j;
-          if (q >= hi) break;
-          const uint32_t kj = key_of(sc.A[q]);
-          r += (kj > k || (kj == k && q < pos)) ? 1 : 0;
+          const uint32_t kj = keys[2 * min(q, 64 * S - 1) + 1];
+          r += (q < hi && (kj > k || (kj == k && q < pos))) ? 1 : 0;
         }
         dst[s] = lo + r;
       }
@@ -183,10 +185,82 @@ __device__ void lds_segment_sort(const TopkLdsV2& sc, int m, int maxlen, int lan
   wave_lds_sync();
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// A register window over positions [base, base + 64) of the row: lane i holds
+// position base + i.  Once an introselect / introsort range fits 64 positions,
+// every later range of that chain is a sub-range, so the steps run on the
+// window without LDS loads or write-backs; flush() stores it back.
+struct TopkWindow {
+  int base;  // -1: no window
+  uint64_t w;
+  __device__ __forceinline__ void load(const TopkLdsV2& sc, int b, int n, int lane) {
+    base = b;
+    w = b + lane < n ? sc.A[b + lane] : 0ull;
+  }
+  __device__ __forceinline__ void flush(const TopkLdsV2& sc, int n, int lane) {
+    if (base >= 0) {
+      if (base + lane < n) sc.A[base + lane] = w;
+      wave_lds_sync();
+      base = -1;
+    }
+  }
+  __device__ __forceinline__ bool covers(int f, int l) const { return base >= 0 && f >= base && l <= base + 64; }
+};
+
+// __unguarded_partition_pivot(first, last) on the window (same rule as lds_partition)
+__device__ __forceinline__ int win_partition(TopkWindow& win, int first, int last, const TopkLdsV2& sc, int lane) {
+  const int base = win.base;
+  const int len = last - first, mid = first + len / 2;
+  const uint32_t hi = (uint32_t)(win.w >> 32);
+  const uint32_t ka = (uint32_t)__builtin_amdgcn_readlane((int)hi, first + 1 - base);
+  const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)hi, mid - base);
+  const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)hi, last - 1 - base);
+  int m;  // __move_median_to_first(first, first+1, mid, last-1)
+  if (ka > kb) {
+    if (kb > kc) m = mid;
+    else if (ka > kc) m = last - 1;
+    else m = first + 1;
+  } else if (ka > kc) m = first + 1;
+  else if (kb > kc) m = last - 1;
+  else m = mid;
+  const uint32_t p = m == first + 1 ? ka : (m == mid ? kb : kc);
+  const uint64_t vf = readlane64(win.w, first - base), vm = readlane64(win.w, m - base);
+  const int pos = base + lane;
+  uint64_t v = pos == first ? vm : (pos == m ? vf : win.w);  // iter_swap(first, m)
+  const uint32_t k = key_of(v);
+  const bool in = pos >= first && pos < last;
+  const bool isl = in && pos > first && !(k > p);
+  const bool isr = in && !(p > k);
+  const uint64_t Lb = __ballot(isl), Rb = __ballot(isr);
+  const int a = (int)mbcnt(Lb);
+  const int bgt = (int)__popcll(Rb) - (int)mbcnt(Rb) - (isr ? 1 : 0);
+  const bool swl = isl && bgt > a, swr = isr && a > bgt;
+  const uint64_t SWL = __ballot(swl), SWR = __ballot(swr);
+  if (SWL) {  // exchange the t-th swapping left stop with the t-th swapping right stop
+    const int rank = swl ? a : bgt;
+    if (swl) sc.xa[rank] = v;
+    if (swr) sc.xb[rank] = v;
+    wave_lds_sync();
+    if (swl) v = sc.xb[rank];
+    if (swr) v = sc.xa[rank];
+    wave_lds_sync();
+  }
+  win.w = v;
+  const uint64_t nsl = Lb & ~SWL;
+  const int c1 = nsl ? base + __ffsll((unsigned long long)nsl) - 1 : (1 << 30);
+  const int c2 = SWR ? base + __ffsll((unsigned long long)SWR) - 1 : last;
+  return c1 < c2 ? c1 : c2;
+}
+
 // std::nth_element(begin, begin+k-1, end) -- or, when k*64 <= n, the whole
 // std::partial_sort(begin, begin+k, end).  Returns true when [0, k) is final.
 template <int S>
-__device__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
+__device__ __forceinline__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
   uint64_t* A = sc.A;
   if (k <= 0) return true;
   if (k * 64 <= n) {  // std::partial_sort(begin, begin+k, end)
@@ -201,8 +275,10 @@ __device__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
   int first = 0, last = n;
   const int nth = k - 1;
   int depth = 2 * ilog2(n);
+  TopkWindow win{-1, 0ull};
   while (last - first > 3) {
     if (depth == 0) {
+      win.flush(sc, n, lane);
       if (lane == 0) {
         s_heap_select(A, first, nth + 1, last);
         const uint64_t t = A[first];
@@ -213,10 +289,20 @@ __device__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
       return false;
     }
     --depth;
-    const int cut = lds_partition_any<S>(sc, first, last, lane);
+    int cut;
+    if (last - first <= 64) {
+      if (!win.covers(first, last)) {
+        win.flush(sc, n, lane);
+        win.load(sc, first, n, lane);
+      }
+      cut = win_partition(win, first, last, sc, lane);
+    } else {
+      cut = lds_partition_any<S>(sc, first, last, lane);
+    }
     if (cut <= nth) first = cut;
     else last = cut;
   }
+  win.flush(sc, n, lane);
   if (last - first > 1) {  // __insertion_sort(first, last): <= 3 elements, stable
     if (lane == 0) {
       for (int i = first + 1; i < last; ++i) {
@@ -236,13 +322,14 @@ __device__ bool lds_select(const TopkLdsV2& sc, int n, int k, int lane) {
 
 // std::sort(begin, begin+m): __introsort_loop + __final_insertion_sort
 template <int S>
-__device__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
+__device__ __forceinline__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
   uint64_t* A = sc.A;
   if (m <= 1) return;
   // every position starts in its own (trivial) segment
   for (int pos = lane; pos < m; pos += 64) sc.seg[pos] = (uint32_t)pos | ((uint32_t)(pos + 1) << 16);
   int sp = 0;
   sc.stk[sp++] = 0 | (m << 10) | ((2 * ilog2(m)) << 20);
+  TopkWindow win{-1, 0ull};
   while (sp > 0) {
     --sp;
     const int e = sc.stk[sp];
@@ -252,6 +339,7 @@ __device__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
     bool heaped = false;
     while (l - f > 16) {
       if (d == 0) {  // std::__partial_sort(f, l, l): heapsort leaves [f, l) sorted
+        win.flush(sc, m, lane);
         if (lane == 0) {
           s_heap_select(A, f, l, l);
           s_sort_heap(A, f, l);
@@ -261,7 +349,17 @@ __device__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
         break;
       }
       --d;
-      const int cut = lds_partition_any<S>(sc, f, l, lane);
+      int cut;
+      if (l - f <= 64) {
+        if (!win.covers(f, l)) {
+          win.flush(sc, m, lane);
+          win.load(sc, f, m, lane);
+        }
+        cut = win_partition(win, f, l, sc, lane);
+      } else {
+        win.flush(sc, m, lane);
+        cut = lds_partition_any<S>(sc, f, l, lane);
+      }
       if (lane == 0) sc.stk[sp] = cut | (l << 10) | (d << 20);
       ++sp;
       wave_lds_sync();
@@ -270,15 +368,194 @@ __device__ void lds_sort_prefix(const TopkLdsV2& sc, int m, int lane) {
     if (!heaped && l - f > 1)
       for (int pos = f + lane; pos < l; pos += 64) sc.seg[pos] = (uint32_t)f | ((uint32_t)l << 16);
   }
+  win.flush(sc, m, lane);
   wave_lds_sync();
-  lds_segment_sort<S>(sc, m, 16, lane);
+  lds_segment_sort<S>(sc, m, lane);
+}
+
+// std::sort(begin, begin+m) for m > 64, level-parallel.  __introsort_loop's
+// pending segments are disjoint and each partition / heapsort moves elements only
+// inside its own segment, so the order in which the stack processes them does not
+// matter: here all segments of one recursion level are partitioned in one
+// wave-wide step (segmented ranks: prefix counts of the stop flags, differenced
+// at the segment ends; pairs exchanged through xa / xb at index f/2 + rank, which
+// stays inside the segment's own share).  Each position carries its segment
+// [f, l) and depth budget d.  Then __final_insertion_sort as the segment sort.
+template <int S>
+__device__ __forceinline__ void lds_sort_prefix_par(const TopkLdsV2& sc, int m, int lane, int dbg = 0) {
+  uint64_t* A = sc.A;
+  uint32_t* PLR = sc.seg;                               // prefix counts (left | right << 16), then segments
+  uint32_t* CUT = reinterpret_cast<uint32_t*>(sc.xa);   // per segment start: min cut candidate
+  int f[S], l[S], d[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    f[s] = 0;
+    l[s] = m;
+    d[s] = 2 * ilog2(m);
+  }
+  while (true) {
+    bool act[S], heap[S];
+    uint64_t any_act = 0ull, any_heap = 0ull;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      const bool big = pos < m && l[s] - f[s] > 16;
+      act[s] = big && d[s] > 0;
+      heap[s] = big && d[s] == 0;
+      any_act |= __ballot(act[s]);
+      any_heap |= __ballot(heap[s]);
+    }
+    if (!any_act && !any_heap) break;
+    if (any_heap) {  // std::__partial_sort(f, l, l) per exhausted segment, serial, one lane each
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (heap[s] && 64 * s + lane == f[s]) {
+          s_heap_select(A, f[s], l[s], l[s]);
+          s_sort_heap(A, f[s], l[s]);
+        }
+        if (heap[s]) {  // sorted: final, a trivial segment for the insertion sort
+          f[s] = 64 * s + lane;
+          l[s] = f[s] + 1;
+        }
+      }
+      wave_lds_sync();
+    }
+    if (!any_act) continue;
+    // ---- __unguarded_partition_pivot on every active segment ----------------
+    uint64_t v[S];
+    uint32_t p[S];
+    bool isl[S], isr[S];
+    int mp[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      v[s] = pos < m ? A[pos] : 0ull;
+      p[s] = 0u;
+      mp[s] = -1;
+      if (act[s]) {
+        const int mid = f[s] + (l[s] - f[s]) / 2;
+        const uint32_t ka = key_of(A[f[s] + 1]), kb = key_of(A[mid]), kc = key_of(A[l[s] - 1]);
+        int mm;
+        if (ka > kb) {
+          if (kb > kc) mm = mid;
+          else if (ka > kc) mm = l[s] - 1;
+          else mm = f[s] + 1;
+        } else if (ka > kc) mm = f[s] + 1;
+        else if (kb > kc) mm = l[s] - 1;
+        else mm = mid;
+        p[s] = mm == f[s] + 1 ? ka : (mm == mid ? kb : kc);
+        mp[s] = mm;
+        if (pos == f[s]) v[s] = A[mm];  // iter_swap(first, median)
+        else if (pos == mm) v[s] = A[f[s]];
+      }
+    }
+    int totL = 0, totR = 0;
+    int pl[S], pr[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      const uint32_t k = key_of(v[s]);
+      isl[s] = act[s] && pos > f[s] && !(k > p[s]);
+      isr[s] = act[s] && !(p[s] > k);
+      const uint64_t Lb = __ballot(isl[s]), Rb = __ballot(isr[s]);
+      pl[s] = totL + (int)mbcnt(Lb);
+      pr[s] = totR + (int)mbcnt(Rb);
+      totL += (int)__popcll(Lb);
+      totR += (int)__popcll(Rb);
+    }
+    wave_lds_sync();  // the median / first reads above are done before any write
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (pos < m) PLR[pos] = (uint32_t)pl[s] | ((uint32_t)pr[s] << 16);
+      if (act[s] && pos == f[s]) CUT[pos] = (uint32_t)l[s];
+    }
+    if (lane == 0) PLR[m] = (uint32_t)totL | ((uint32_t)totR << 16);
+    wave_lds_sync();
+    bool swl[S], swr[S];
+    int xi[S];
+    uint64_t any_sw = 0ull;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      swl[s] = swr[s] = false;
+      xi[s] = 0;
+      if (act[s]) {
+        const int a = pl[s] - (int)(PLR[f[s]] & 0xFFFFu);
+        const int bgt = (int)(PLR[l[s]] >> 16) - pr[s] - (isr[s] ? 1 : 0);
+        swl[s] = isl[s] && bgt > a;
+        swr[s] = isr[s] && a > bgt;
+        xi[s] = f[s] / 2 + (swl[s] ? a : bgt);
+      }
+      any_sw |= __ballot(swl[s] || swr[s]);
+    }
+    // the write of the swapped / pivot-moved values happens after the exchange
+    if (any_sw) {
+      uint64_t* XA = sc.xa;
+      uint64_t* XB = sc.xb;
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (swl[s]) XA[xi[s]] = v[s];
+        if (swr[s]) XB[xi[s]] = v[s];
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (swl[s]) v[s] = XB[xi[s]];
+        if (swr[s]) v[s] = XA[xi[s]];
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        if (act[s] && pos == f[s]) CUT[pos] = (uint32_t)l[s];  // CUT aliases XA: re-initialise
+      }
+      wave_lds_sync();
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (act[s]) {
+        A[pos] = v[s];
+        // cut = min(first non-swapping left stop, lowest swapping right stop | last)
+        if ((isl[s] && !swl[s]) || swr[s]) atomicMin(&CUT[f[s]], (uint32_t)pos);
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (act[s]) {
+        const int cut = (int)CUT[f[s]];
+        if (pos < cut) l[s] = cut;
+        else f[s] = cut;
+        d[s] -= 1;
+      }
+    }
+    wave_lds_sync();
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = 64 * s + lane;
+    if (pos < m) sc.seg[pos] = (uint32_t)f[s] | ((uint32_t)l[s] << 16);
+  }
+  wave_lds_sync();
+  if (!(dbg & 32)) lds_segment_sort<S>(sc, m, lane);
+}
+
+// std::sort(begin, begin+m): the windowed sequential introsort for short prefixes,
+// the level-parallel one when the prefix spans several slots
+template <int S>
+__device__ __forceinline__ void lds_sort_head(const TopkLdsV2& sc, int m, int lane, int dbg = 0) {
+  if (S > 1 && m > 64) lds_sort_prefix_par<S>(sc, m, lane, dbg);
+  else lds_sort_prefix<S>(sc, m, lane);
 }
 
 // Full top-k of the row in sc.A[0, n) (TopKImpl.h:45-86).  On return positions
 // [0, k) hold torch's order.
 template <int S>
-__device__ void lds_topk(const TopkLdsV2& sc, int n, int k, int lane) {
-  if (!lds_select<S>(sc, n, k, lane)) lds_sort_prefix<S>(sc, k - 1, lane);
+__device__ __forceinline__ void lds_topk(const TopkLdsV2& sc, int n, int k, int lane) {
+  if (!lds_select<S>(sc, n, k, lane)) lds_sort_head<S>(sc, k - 1, lane);
 }
 
 }  // namespace mxa

@@ -239,9 +239,9 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
         assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
 
 
-def _attn_both_paths(M, q, k, v, scale, **kw):
-    """Run the fused op on the row-oriented kernel (default) and on the MFMA
-    score-tile kernel (MXA_ATTN_PATH=tiles)."""
+def _attn_all_paths(M, q, k, v, scale, **kw):
+    """Run the fused op on the row kernel (default) and on the MFMA score-tile
+    kernel (MXA_ATTN_PATH=tiles)."""
     res = []
     for path in (None, "tiles"):
         if path:
@@ -276,7 +276,7 @@ def test_expred_rows_and_tiles_paths_vs_oracle(M, D, N, T, k):
     kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
     v = rng.standard_normal((B, H, T, D), dtype=np.float32)
     scale = float(D) ** -0.5
-    rows, tiles = _attn_both_paths(M, q, kk, v, scale, k_top=k)
+    rows, tiles = _attn_all_paths(M, q, kk, v, scale, k_top=k)
     r = O.attention(q, kk, v, scale, k_top=k)
     _check_vs_oracle(rows, r, "rows")
     _check_vs_oracle(tiles, r, "tiles")
@@ -298,10 +298,26 @@ def test_expred_special_rows(M):
     q[1, 1, 17, :] *= np.float32(2.0 ** 100)    # true scores overflow for this row
     kk[1, 1, :, :] *= np.float32(2.0 ** 30)
     q[1, 2, :4, :] = 0.0                        # zero query rows (all preds tie)
-    rows, tiles = _attn_both_paths(M, q, kk, v, 0.125, k_top=k)
+    rows, tiles = _attn_all_paths(M, q, kk, v, 0.125, k_top=k)
     r = O.attention(q, kk, v, 0.125, k_top=k)
     _check_vs_oracle(rows, r, "rows")
     _check_vs_oracle(tiles, r, "tiles")
+
+
+@pytest.mark.parametrize("mode", ["MXINT4", "two_step_leading_ones", "partial_Q", "partial_K"])
+@pytest.mark.parametrize("N,T,k", [(197, 197, 20), (77, 120, 77), (33, 256, 154)])
+def test_approx_modes_all_paths_vs_oracle(M, mode, N, T, k):
+    """Approximator-code scoring (v_dot4, EXP / EXION-MUL block combine) on both
+    fused kernels, odd row counts."""
+    rng = np.random.default_rng(7)
+    B, H, D = 1, 2, 72
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    outs = _attn_all_paths(M, q, kk, v, 72 ** -0.5, k_top=k, pred_mode=mode)
+    r = O.attention(q, kk, v, 72 ** -0.5, k_top=k, pred_mode=mode)
+    for got, name in zip(outs, ("rows", "tiles")):
+        _check_vs_oracle(got, r, name)
 
 
 def test_pixart_cross_full_batch(M):

@@ -12,6 +12,6 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
   i=$((i+1))
   rm -rf gpurun_out/pmc_$CFG_$i
   timeout -k 10 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_${CFG}_$i -o p --output-format csv -- \
-      python tools/probe_attn.py $CFG > gpurun_out/pmc_${CFG}_$i.log 2>&1 || exit $?
+      python tools/probe_attn.py $CFG ${PATHS:-rows,tiles} > gpurun_out/pmc_${CFG}_$i.log 2>&1 || exit $?
 done
 echo pmc done

@@ -1,0 +1,17 @@
+"""One fused call on a bench config (for rocprofv3 --pmc with MXA_LIB / MXA_DBG_SKIP)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+import mx_quantization_amd as M
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "deit_base"
+B, H, N, D, k = {"deit_base": (256, 12, 197, 64, 20), "dit_xl2": (64, 16, 256, 72, 154)}[cfg]
+q, kk, v = (torch.from_numpy(np.random.default_rng(s).standard_normal((B, H, N, D), dtype=np.float32)).cuda()
+            for s in range(3))
+for _ in range(2):
+    M.mx_topk_attention(q, kk, v, D ** -0.5, k_top=k)
+torch.cuda.synchronize()
