@@ -573,6 +573,10 @@ __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs 
   MXA_PHASE_FLUSH();
 }
 
+}  // namespace mxa
+#include "mxa_rows2.hpp"
+namespace mxa {
+
 struct PVArgs {
   const int8_t* pc;
   const int16_t* ps;
@@ -633,6 +637,37 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(TopkArgs a) {
     const uint32_t ix = (uint32_t)sc.A[pos];
     a.out_idx[row * a.k + pos] = (int64_t)ix;
     if (a.out_vals) a.out_vals[row * a.k + pos] = src[ix];
+  }
+}
+
+// register-resident top-k (mxa_topk_reg.hpp)
+template <int S>
+__global__ __launch_bounds__(256) void topk_reg_kernel(TopkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= a.rows) return;  // wave-uniform
+  RegTopk<S> tk;
+  tk.init(smem + (size_t)wave * topk_scratch_bytes(S), a.n, lane);
+  const float* src = a.vals + row * a.ld;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = 64 * s + lane;
+    tk.K[s] = pos < a.n ? order_key(src[pos]) : 0u;
+    tk.I[s] = (uint32_t)pos;
+  }
+  tk.run(a.k);
+  tk.finalize();
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int pos = 64 * s + lane;
+    if (64 * s < a.k) {
+      const uint32_t ix = tk.out_idx(s);
+      if (pos < a.k) {
+        a.out_idx[row * a.k + pos] = (int64_t)ix;
+        if (a.out_vals) a.out_vals[row * a.k + pos] = src[ix];
+      }
+    }
   }
 }
 
@@ -839,6 +874,65 @@ static int launch_rows(const RowsArgs& ra, int mode, int S, int BH, hipStream_t 
   }
 }
 
+// ---- fused row kernel v2 (mxa_rows2.hpp) -----------------------------------
+static size_t rows2_total(int mode, bool topk, const Rows2Args& ra, int S, int W) {
+  return rows2_lds(mode, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, S, ra.tpad, topk ? ra.k_top : 0, W).total;
+}
+// waves per workgroup: two 8-wave workgroups per CU when they fit, else one 16-wave one
+static int rows2_waves(int mode, bool topk, const Rows2Args& ra, int S) {
+  const char* env = getenv("MXA_ROWS2_WAVES");
+  if (env) {
+    const int w = atoi(env);
+    return rows2_total(mode, topk, ra, S, w) <= 160 * 1024 ? w : 0;
+  }
+  if (rows2_total(mode, topk, ra, S, 8) <= 80 * 1024) return 8;
+  if (rows2_total(mode, topk, ra, S, 16) <= 160 * 1024) return 16;
+  if (rows2_total(mode, topk, ra, S, 8) <= 160 * 1024) return 8;
+  if (rows2_total(mode, topk, ra, S, 4) <= 160 * 1024) return 4;
+  return 0;
+}
+
+template <int S, int MODE, bool TOPK, bool BIG>
+static int launch_rows2_b(const Rows2Args& ra0, int BH, hipStream_t stream) {
+  Rows2Args ra = ra0;
+  ra.waves = rows2_waves(MODE, TOPK, ra, S);
+  if (ra.waves <= 0) return MXA_ERR_UNSUPPORTED;
+  const size_t lds = rows2_total(MODE, TOPK, ra, S, ra.waves);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows2_kernel<S, MODE, TOPK, BIG>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL((attn_rows2_kernel<S, MODE, TOPK, BIG>), dim3((unsigned)BH), dim3(64 * ra.waves), lds, stream,
+                     ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+// BIG: a sorted prefix longer than 64 is possible (k > 65)
+template <int S, int MODE, bool TOPK>
+static int launch_rows2_s(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (TOPK && ra.k_top > 65) return launch_rows2_b<S, MODE, TOPK, true>(ra, BH, stream);
+  return launch_rows2_b<S, MODE, TOPK, false>(ra, BH, stream);
+}
+
+template <int S>
+static int launch_rows2_mode(const Rows2Args& ra, int mode, bool topk, int BH, hipStream_t stream) {
+  if (!topk) return launch_rows2_s<S, kModeTrue, false>(ra, BH, stream);
+  switch (mode) {
+    case kModeOpExp: return launch_rows2_s<S, kModeOpExp, true>(ra, BH, stream);
+    case kModeOpMul: return launch_rows2_s<S, kModeOpMul, true>(ra, BH, stream);
+    case kModeExSign: return launch_rows2_s<S, kModeExSign, true>(ra, BH, stream);
+    default: return launch_rows2_s<S, kModeTrue, true>(ra, BH, stream);
+  }
+}
+
+static int launch_rows2(const Rows2Args& ra, int mode, bool topk, int S, int BH, hipStream_t stream) {
+  switch (S) {
+    case 1: return launch_rows2_mode<1>(ra, mode, topk, BH, stream);
+    case 2: return launch_rows2_mode<2>(ra, mode, topk, BH, stream);
+    case 4: return launch_rows2_mode<4>(ra, mode, topk, BH, stream);
+    default: return launch_rows2_mode<8>(ra, mode, topk, BH, stream);
+  }
+}
+
 static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev) {
   if (!p || !p->q || !p->k || !p->v || !p->out) return MXA_ERR_ARG;
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
@@ -870,9 +964,16 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
                         : p->pred_mode == MXA_PRED_EXION   ? kModeOpMul
                                                            : kModeOpExp;
   const char* path_env = getenv("MXA_ATTN_PATH");
-  const bool rows_path = L.nbd <= kMaxNB &&
-                         rows_lds(rows_mode, p->T, kst, L.nbd, rows_S, L.tpad, p->top_k != 0).total <= 160 * 1024 &&
-                         !(path_env && std::string(path_env) == "tiles");
+  const std::string path = path_env ? path_env : "";
+  Rows2Args r2{};
+  r2.T = p->T; r2.D = p->D; r2.nbd = L.nbd; r2.ntb = L.ntb; r2.tpad = L.tpad; r2.k_top = p->k_top;
+  r2.kst = kst; r2.vst = L.tpad + 16;
+  const bool rows2_path = L.nbd <= kMaxNB && path != "tiles" && path != "rows1" &&
+                          rows2_waves(rows_mode, p->top_k != 0, r2, rows_S) > 0;
+  const bool rows_path = rows2_path ||
+                         (L.nbd <= kMaxNB &&
+                          rows_lds(rows_mode, p->T, kst, L.nbd, rows_S, L.tpad, p->top_k != 0).total <= 160 * 1024 &&
+                          path != "tiles");
   // the ex_pred rows kernel derives the sign operand from the MX codes
   const bool need_op = need_pred && !(rows_path && rows_mode == kModeExSign);
 
@@ -935,7 +1036,27 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   sa.idx_out = p->idx_out; sa.true_out = p->true_out; sa.pred_out = p->pred_out;
   sa.pc = reinterpret_cast<int8_t*>(ws + L.pc);
   sa.ps = reinterpret_cast<int16_t*>(ws + L.ps);
-  if (rows_path) {
+  if (rows2_path) {
+    r2.qc = sa.qc; r2.qop = sa.qop; r2.qsT = sa.qsT; r2.qsA = sa.qsA;
+    r2.qsg = reinterpret_cast<const uint32_t*>(ws + L.qsg);
+    r2.kc = sa.kc; r2.kop = sa.kop; r2.ksT = sa.ksT; r2.ksA = sa.ksA;
+    r2.ksg = reinterpret_cast<const uint32_t*>(ws + L.ksg);
+    r2.vt = reinterpret_cast<const int8_t*>(ws + L.vt);
+    r2.vs = reinterpret_cast<const int16_t*>(ws + L.vs);
+    r2.B = p->B; r2.H = p->H; r2.N = p->N; r2.dpad = L.dpad;
+    r2.bfloat = p->bfloat; r2.flush_p = p->flush_subnormals; r2.scale = p->scale;
+    r2.bias = p->bias;
+    r2.bs0 = p->bias_strides[0]; r2.bs1 = p->bias_strides[1]; r2.bs2 = p->bias_strides[2]; r2.bs3 = p->bias_strides[3];
+    r2.out = p->out; r2.os0 = p->out_strides[0]; r2.os1 = p->out_strides[1]; r2.os2 = p->out_strides[2];
+    r2.idx_out = p->idx_out; r2.true_out = p->true_out; r2.pred_out = p->pred_out;
+    rc = launch_rows2(r2, rows_mode, p->top_k != 0, rows_S, (int)BH, stream);
+    if (rc) return rc;
+    if (ev) {
+      (void)hipEventRecord(ev[4], stream);
+      (void)hipEventRecord(ev[5], stream);
+    }
+    return MXA_OK;
+  } else if (rows_path) {
     RowsArgs ra{};
     ra.s = sa;
     ra.qsg = reinterpret_cast<const uint32_t*>(ws + L.qsg);
@@ -997,10 +1118,14 @@ extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream,
 template <int S>
 static int launch_topk(const TopkArgs& ta, hipStream_t stream) {
   const dim3 grid((unsigned)((ta.rows + 3) / 4));
-  if (getenv("MXA_TOPK_V1"))
+  const char* env = getenv("MXA_TOPK_IMPL");
+  const std::string impl = env ? env : "";
+  if (impl == "v1")
     hipLaunchKernelGGL(topk_rows_v1_kernel<S>, grid, dim3(256), (size_t)4 * (2 * 64 * S + kTopkStack / 2) * 8, stream, ta);
-  else
+  else if (impl == "lds")
     hipLaunchKernelGGL(topk_rows_kernel<S>, grid, dim3(256), (size_t)4 * topk_scratch_bytes(S), stream, ta);
+  else
+    hipLaunchKernelGGL(topk_reg_kernel<S>, grid, dim3(256), (size_t)4 * topk_scratch_bytes(S), stream, ta);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 

@@ -1,0 +1,415 @@
+// Row-oriented fused attention kernel, version 2: scores -> exact-order top-k ->
+// softmax -> P quantization -> P.V, one wave per query row, nothing of the row
+// leaves the CU but the output and the kept indices.
+//
+// Per workgroup (one head): the head's K tables (MXINT8 codes + exponents, the
+// approximator operands) and V^T codes + exponents are staged in LDS once.  Per
+// query row (one wave):
+//   1. the T approximate (or true) scores land in registers in position order
+//      (lane i, slot s <-> key 64 s + i) -- exact fp64 block epilogue;
+//   2. RegTopk (mxa_topk_reg.hpp) reproduces torch's CPU topk index order;
+//   3. lane l < k recomputes the true score of the l-th kept key (v_dot4 over the
+//      LDS codes), softmax over the kept scores (DPP reductions);
+//   4. P is MX-quantized along keys (block maxima by LDS atomic max) into a dense
+//      LDS code row that holds zeros everywhere else;
+//   5. out[d] = sum_b 2^(eP_b + eV_bd) * sum_{t in b} P_t V_td: v_dot4 of the P row
+//      (broadcast reads) against lane d's V^T row, exact fp64 block epilogue.
+// Callers: workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
+// workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859; the MX matmul
+// of P.V: microxscaling/mx/matmul.py:68-76.
+#pragma once
+#include "mxa_topk_reg.hpp"
+
+namespace mxa {
+
+struct Rows2Args {
+  // query side (rows_prep outputs)
+  const int8_t *qc, *qop;
+  const int16_t *qsT, *qsA;
+  const uint32_t* qsg;
+  // key side
+  const int8_t *kc, *kop;
+  const int16_t *ksT, *ksA;
+  const uint32_t* ksg;
+  // value side (cols_prep outputs: V^T codes [BH][D][tpad], exps [BH][ntb][D])
+  const int8_t* vt;
+  const int16_t* vs;
+  int B, H, N, T, D, nbd, dpad, ntb, tpad;
+  int kst, vst;  // LDS row strides of the K code tables and the V^T table
+  int k_top, bfloat, flush_p;
+  float scale;
+  const float* bias;
+  int64_t bs0, bs1, bs2, bs3;
+  float* out;
+  int64_t os0, os1, os2;
+  int64_t* idx_out;
+  float* true_out;
+  float* pred_out;
+  int waves;  // waves per workgroup
+};
+
+struct Rows2Lds {
+  size_t mx, sT, op, sA, sg, vt, vs, waves, per_wave, total;
+};
+
+__host__ __device__ inline size_t r2_al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline Rows2Lds rows2_lds(int mode, int T, int D, int kst, int nbd, int vst, int ntb, int S,
+                                              int tpad, int k_top, int waves) {
+  Rows2Lds L;
+  size_t o = 0;
+  L.mx = o;
+  o += r2_al16((size_t)T * kst);
+  L.sT = o;
+  o += r2_al16((size_t)T * nbd * 2);
+  L.op = o;
+  if (mode == kModeOpExp || mode == kModeOpMul) o += r2_al16((size_t)T * kst);
+  L.sA = o;
+  if (mode != kModeTrue) o += r2_al16((size_t)T * nbd * 2);
+  L.sg = o;
+  if (mode == kModeExSign) o += r2_al16((size_t)T * nbd * 4);
+  L.vt = o;
+  o += r2_al16((size_t)D * vst);
+  L.vs = o;
+  o += r2_al16((size_t)ntb * D * 2);
+  L.waves = o;
+  // top-k scratch (mxa_topk_lds.hpp layout), the P code row, P block exponents
+  // and block maxima (16 each)
+  L.per_wave = r2_al16(topk_scratch_bytes(S)) + r2_al16((size_t)tpad) + 64 + 64;
+  L.total = o + (size_t)waves * L.per_wave;
+  return L;
+}
+
+// the true score of key row krow (MXINT8 codes in LDS, exponents kexp) against the
+// uniform query codes qw / exponents qe: fl32(exact sum) * scale, bfloat-rounded
+template <int MUL>
+__device__ __forceinline__ double r2_dot(const int8_t* qrow, const int16_t* qs, int64_t qs0, int nbd,
+                                         const int8_t* krow, const int16_t* kexp, bool& nan) {
+  double acc = 0.0;
+#pragma unroll
+  for (int b = 0; b < kMaxNB; ++b) {
+    if (b < nbd) {
+      const cu32 src = (cu32)(qrow + 32 * b);  // scalar loads: 8 SGPRs live per block
+      uint32_t qw[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) qw[c] = src[c];
+      const int qe = s_exp16(qs, qs0 + b);
+      const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
+      int I = 0;
+      I = __builtin_amdgcn_sdot4((int)qw[0], (int)x0.x, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[1], (int)x0.y, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[2], (int)x0.z, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[3], (int)x0.w, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[4], (int)x1.x, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[5], (int)x1.y, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[6], (int)x1.z, I, false);
+      I = __builtin_amdgcn_sdot4((int)qw[7], (int)x1.w, I, false);
+      const int e = exp_from16(kexp[b]);
+      if (e == kExpNaN || qe == kExpNaN) nan = true;
+      else if (MUL) acc += (double)I * (double)(qe * e) * (1.0 / 4096.0);
+      else acc += (double)I * pow2d(qe + e);
+    }
+  }
+  return acc;
+}
+
+template <int S, int MODE, bool TOPK, bool BIG>
+__global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x;
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, vst = a.vst, ntb = a.ntb;
+  const int b_ = bh / a.H, h_ = bh % a.H;
+  const Rows2Lds L = rows2_lds(MODE, T, D, kst, nbd, vst, ntb, S, a.tpad, TOPK ? a.k_top : 0, a.waves);
+  int8_t* tmx = reinterpret_cast<int8_t*>(smem + L.mx);
+  int16_t* tsT = reinterpret_cast<int16_t*>(smem + L.sT);
+  int8_t* top = reinterpret_cast<int8_t*>(smem + L.op);
+  int16_t* tsA = reinterpret_cast<int16_t*>(smem + L.sA);
+  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
+  int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
+  int16_t* tvs = reinterpret_cast<int16_t*>(smem + L.vs);
+  unsigned char* wbase = smem + L.waves + (size_t)wave * L.per_wave;
+  const size_t tkb = topk_scratch_bytes(S);
+  int8_t* prow = reinterpret_cast<int8_t*>(wbase + r2_al16(tkb));
+  int* pe = reinterpret_cast<int*>(wbase + r2_al16(tkb) + r2_al16(a.tpad));
+  uint32_t* bm = reinterpret_cast<uint32_t*>(pe + 16);
+
+  // ---- stage the head's K and V tables ---------------------------------------
+  const int64_t kb = (int64_t)bh * T;
+  {
+    const int cpr = a.dpad / 16;
+    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+      const int j = i / cpr, c = i - j * cpr;
+      *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
+          *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
+      if (kOp)
+        *reinterpret_cast<uint4*>(top + (size_t)j * kst + 16 * c) =
+            *reinterpret_cast<const uint4*>(a.kop + (kb + j) * a.dpad + 16 * c);
+    }
+    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
+      tsT[i] = a.ksT[kb * nbd + i];
+      if (MODE != kModeTrue) tsA[i] = a.ksA[kb * nbd + i];
+      if (MODE == kModeExSign) tsg[i] = a.ksg[kb * nbd + i];
+    }
+    const int vpr = a.tpad / 16;
+    const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
+    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
+      const int d = i / vpr, c = i - d * vpr;
+      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
+          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+    }
+    const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
+    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];
+    for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(prow)[c] = 0u;
+    if (lane < 16) bm[lane] = 0u;
+  }
+  __syncthreads();
+
+  for (int r = __builtin_amdgcn_readfirstlane(wave); r < a.N; r += a.waves) {
+    const int64_t grow = (int64_t)bh * a.N + r;
+    const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
+
+    const int8_t* qmx = a.qc + grow * a.dpad;
+
+    // ---- the row's T values in position order ------------------------------
+    float vals[S];
+    if constexpr (MODE == kModeExSign) {
+      // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
+      uint32_t sq[kMaxNB];
+      int eq[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) {
+        sq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
+        eq[b] = b < nbd ? s_exp16(a.qsA, grow * nbd + b) : 0;
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = 64 * s + lane;
+        double acc = 0.0;
+        bool nan = false;
+        if (j < T) {
+#pragma unroll
+          for (int b = 0; b < kMaxNB; ++b) {
+            if (b < nbd) {
+              const int e = exp_from16(tsA[j * nbd + b]);
+              if (e == kExpNaN || eq[b] == kExpNaN) nan = true;
+              const int m = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
+              acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
+            }
+          }
+        }
+        vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+      }
+    } else if constexpr (kOp) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = min(64 * s + lane, T - 1);
+        bool nan = false;
+        const double acc = r2_dot<MODE == kModeOpMul>(a.qop + grow * a.dpad, a.qsA, grow * nbd, nbd, top + (size_t)j * kst, tsA + j * nbd, nan);
+        vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = min(64 * s + lane, T - 1);
+        bool nan = false;
+        const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
+        // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
+        vals[s] = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int j = 64 * s + lane;
+      if (j < T) {
+        if (brow) vals[s] = vals[s] + brow[(int64_t)j * a.bs3];
+        if (MODE == kModeTrue) {
+          if (a.true_out) a.true_out[grow * T + j] = vals[s];
+        } else if (a.pred_out) {
+          a.pred_out[grow * T + j] = vals[s];
+        }
+      }
+    }
+
+    // the true score of key j for this row (bias included)
+    auto true_of = [&](int j, bool& nan) -> float {
+      const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
+      float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
+      if (brow) t = t + brow[(int64_t)j * a.bs3];
+      return t;
+    };
+    if (MODE != kModeTrue && a.true_out) {  // debug output: every key's true score
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = 64 * s + lane;
+        bool nan = false;
+        const float t = true_of(min(j, T - 1), nan);
+        if (j < T) a.true_out[grow * T + j] = t;
+      }
+    }
+
+    int ix[S];
+    bool kept[S];
+    if constexpr (TOPK) {
+      // ---- top-k in torch's CPU order ----------------------------------------
+      RegTopk<S, BIG> tk;
+      tk.init(wbase, T, lane);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        tk.K[s] = order_key(vals[s]);
+        tk.I[s] = (uint32_t)(64 * s + lane);
+      }
+      tk.run(a.k_top);
+      tk.finalize();
+      // ---- vals = true.gather(idx); softmax ----------------------------------
+      float v[S];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        kept[s] = pos < a.k_top;
+        ix[s] = 0;
+        v[s] = -INFINITY;
+        if (64 * s < a.k_top) {
+          ix[s] = kept[s] ? (int)tk.out_idx(s) : 0;
+          if (kept[s]) {
+            if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
+            bool nan = false;
+            v[s] = true_of(ix[s], nan);
+            mx = fmaxf(mx, v[s]);
+          }
+        }
+      }
+      mx = wave_max_f32(mx);
+      float sum = 0.0f;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        v[s] = kept[s] ? expf(v[s] - mx) : 0.0f;
+        sum += v[s];
+      }
+      sum = wave_sum_f32(sum);
+      // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (kept[s]) {
+          v[s] = round_bfloat(v[s] / sum, a.bfloat, kRoundNearest, 1);
+          atomicMax(&bm[ix[s] >> 5], __float_as_uint(v[s]) & 0x7FFFFFFFu);
+        }
+      }
+      wave_lds_sync();
+      if (lane < ntb) {
+        int e_raw;
+        const int es = scale_exponent(bm[lane], 127, &e_raw);
+        const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
+        pe[lane] = es == kExpNaN ? kExpNaN : es - 6;
+        bm[lane] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);  // 0: NaN block
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (kept[s]) {
+          const uint32_t e = bm[ix[s] >> 5];
+          int code = 0;
+          if (e & 0xFFFFu) {
+            const int es = (int)(e & 0xFFFFu) - 1024;
+            const float x = (e & 0x10000u) ? v[s] * 0.0f : v[s];
+            code = (int)round_code(x, es, 8, kRoundNearest);
+          }
+          prow[ix[s]] = (int8_t)code;
+        }
+      }
+      wave_lds_sync();
+      if (lane < 16) bm[lane] = 0u;
+    } else {
+      // ---- dense: attn = softmax(true) over every key (blocks excluded from top-k)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        if (pos >= T) vals[s] = -INFINITY;
+        mx = fmaxf(mx, vals[s]);
+      }
+      mx = wave_max_f32(mx);
+      float sum = 0.0f;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        vals[s] = pos < T ? expf(vals[s] - mx) : 0.0f;
+        sum += vals[s];
+      }
+      sum = wave_sum_f32(sum);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = s * 64 + lane;
+        if (s * 64 >= a.tpad) break;
+        const float x = round_bfloat(vals[s] / sum, a.bfloat, kRoundNearest, 1);
+        const uint32_t mb = half_reduce(__float_as_uint(x) & 0x7FFFFFFFu,
+                                        [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+        int e_raw;
+        const int es = scale_exponent(mb, 127, &e_raw);
+        float xv = x;
+        if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
+        const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+        if (pos < a.tpad) {
+          prow[pos] = (int8_t)code;
+          if ((lane & 31) == 0) pe[pos >> 5] = es == kExpNaN ? kExpNaN : es - 6;
+        }
+      }
+      wave_lds_sync();
+    }
+
+    // ---- out = MX(P) @ MX(V): v_dot4 over 16 keys per read, fp64 block epilogue
+    {
+      double acc[2] = {0.0, 0.0};
+      bool nan[2] = {false, false};
+      const int dsl = D > 64 ? 2 : 1;
+      for (int blk = 0; blk < ntb; ++blk) {
+        const uint4 p0 = *reinterpret_cast<const uint4*>(prow + 32 * blk);
+        const uint4 p1 = *reinterpret_cast<const uint4*>(prow + 32 * blk + 16);
+        const int ep = pe[blk];
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds) {
+          if (ds < dsl) {
+            const int d = min(64 * ds + lane, D - 1);
+            const int8_t* vr = tvt + (size_t)d * vst + 32 * blk;
+            const uint4 x0 = *reinterpret_cast<const uint4*>(vr);
+            const uint4 x1 = *reinterpret_cast<const uint4*>(vr + 16);
+            int I = 0;
+            I = __builtin_amdgcn_sdot4((int)p0.x, (int)x0.x, I, false);
+            I = __builtin_amdgcn_sdot4((int)p0.y, (int)x0.y, I, false);
+            I = __builtin_amdgcn_sdot4((int)p0.z, (int)x0.z, I, false);
+            I = __builtin_amdgcn_sdot4((int)p0.w, (int)x0.w, I, false);
+            I = __builtin_amdgcn_sdot4((int)p1.x, (int)x1.x, I, false);
+            I = __builtin_amdgcn_sdot4((int)p1.y, (int)x1.y, I, false);
+            I = __builtin_amdgcn_sdot4((int)p1.z, (int)x1.z, I, false);
+            I = __builtin_amdgcn_sdot4((int)p1.w, (int)x1.w, I, false);
+            const int ev = exp_from16(tvs[blk * D + d]);
+            if (ep == kExpNaN || ev == kExpNaN) nan[ds] = true;
+            else acc[ds] += (double)I * pow2d(ep + ev);
+          }
+        }
+      }
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const int d = 64 * ds + lane;
+        if (ds < dsl && d < D) {
+          const float o = nan[ds] ? __uint_as_float(0x7FC00000u) : (float)acc[ds];
+          a.out[b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + d] = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+        }
+      }
+    }
+    // ---- restore the all-zero P row for the next query row ------------------
+    wave_lds_sync();
+    if constexpr (TOPK) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        if (64 * s < a.k_top && pos < a.k_top) prow[ix[s]] = 0;
+      }
+    }
+  }
+}
+
+}  // namespace mxa

@@ -110,8 +110,16 @@ def test_exponent_rule_exhaustive_sample(M):
 
 
 # ------------------------------------------------------------------ top-k order
+@pytest.fixture(params=["reg", "lds"])
+def impl(request):
+    """standalone top-k on the register-resident (default) and LDS-resident rows"""
+    os.environ["MXA_TOPK_IMPL"] = request.param
+    yield request.param
+    os.environ.pop("MXA_TOPK_IMPL", None)
+
+
 @pytest.mark.parametrize("name", ["deit", "deit30", "dit", "cross"])
-def test_topk_ties_exact_order(M, name):
+def test_topk_ties_exact_order(M, impl, name):
     d = load("topk_ties.npz")
     k = int(d[f"{name}_k"])
     vals, idx = M.topk(dev(d[f"{name}_pred"]), k)
@@ -120,7 +128,7 @@ def test_topk_ties_exact_order(M, name):
 
 
 @pytest.mark.parametrize("n", [120, 197, 256])
-def test_topk_adversarial_rows(M, n):
+def test_topk_adversarial_rows(M, impl, n):
     d = load("topk_ties.npz")
     rows, ks, want = d[f"adv{n}_rows"], d[f"adv{n}_k"], d[f"adv{n}_idx"]
     for k in np.unique(ks):
@@ -130,7 +138,7 @@ def test_topk_adversarial_rows(M, n):
 
 
 @pytest.mark.parametrize("n,k", [(197, 30), (197, 154), (256, 77), (256, 154), (512, 300), (120, 20), (300, 4)])
-def test_topk_depth_limit_fallbacks_and_partial_sort(M, n, k):
+def test_topk_depth_limit_fallbacks_and_partial_sort(M, impl, n, k):
     rows = np.stack([O.antiqsort_row(n, k)] + [np.random.default_rng(i).integers(0, 3, n).astype(np.float32)
                                                 for i in range(7)])
     _, want = O.topk(rows, k)
@@ -138,7 +146,7 @@ def test_topk_depth_limit_fallbacks_and_partial_sort(M, n, k):
     same(host(idx), want, f"n{n} k{k}")
 
 
-def test_topk_random_small_alphabets_and_specials(M):
+def test_topk_random_small_alphabets_and_specials(M, impl):
     rng = np.random.default_rng(11)
     for n in (5, 17, 64, 65, 127, 128, 129, 197, 256, 300, 511, 512):
         for k in sorted({1, 2, 3, min(n, 20), (n + 1) // 2, n}):
@@ -239,11 +247,15 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
         assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
 
 
+PATHS = ("rows", "rows1", "tiles")
+
+
 def _attn_all_paths(M, q, k, v, scale, **kw):
-    """Run the fused op on the row kernel (default) and on the MFMA score-tile
-    kernel (MXA_ATTN_PATH=tiles)."""
+    """Run the fused op on every kernel path: the row kernel v2 with fused P.V
+    (default), the v1 row kernel + pv_kernel (MXA_ATTN_PATH=rows1) and the MFMA
+    score-tile kernel (MXA_ATTN_PATH=tiles)."""
     res = []
-    for path in (None, "tiles"):
+    for path in (None, "rows1", "tiles"):
         if path:
             os.environ["MXA_ATTN_PATH"] = path
         try:
@@ -276,10 +288,10 @@ def test_expred_rows_and_tiles_paths_vs_oracle(M, D, N, T, k):
     kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
     v = rng.standard_normal((B, H, T, D), dtype=np.float32)
     scale = float(D) ** -0.5
-    rows, tiles = _attn_all_paths(M, q, kk, v, scale, k_top=k)
+    outs = _attn_all_paths(M, q, kk, v, scale, k_top=k)
     r = O.attention(q, kk, v, scale, k_top=k)
-    _check_vs_oracle(rows, r, "rows")
-    _check_vs_oracle(tiles, r, "tiles")
+    for got, name in zip(outs, PATHS):
+        _check_vs_oracle(got, r, name)
 
 
 def test_expred_special_rows(M):
@@ -298,10 +310,10 @@ def test_expred_special_rows(M):
     q[1, 1, 17, :] *= np.float32(2.0 ** 100)    # true scores overflow for this row
     kk[1, 1, :, :] *= np.float32(2.0 ** 30)
     q[1, 2, :4, :] = 0.0                        # zero query rows (all preds tie)
-    rows, tiles = _attn_all_paths(M, q, kk, v, 0.125, k_top=k)
+    outs = _attn_all_paths(M, q, kk, v, 0.125, k_top=k)
     r = O.attention(q, kk, v, 0.125, k_top=k)
-    _check_vs_oracle(rows, r, "rows")
-    _check_vs_oracle(tiles, r, "tiles")
+    for got, name in zip(outs, PATHS):
+        _check_vs_oracle(got, r, name)
 
 
 @pytest.mark.parametrize("mode", ["MXINT4", "two_step_leading_ones", "partial_Q", "partial_K"])
@@ -316,7 +328,7 @@ def test_approx_modes_all_paths_vs_oracle(M, mode, N, T, k):
     v = rng.standard_normal((B, H, T, D), dtype=np.float32)
     outs = _attn_all_paths(M, q, kk, v, 72 ** -0.5, k_top=k, pred_mode=mode)
     r = O.attention(q, kk, v, 72 ** -0.5, k_top=k, pred_mode=mode)
-    for got, name in zip(outs, ("rows", "tiles")):
+    for got, name in zip(outs, PATHS):
         _check_vs_oracle(got, r, name)
 
 
