@@ -54,22 +54,33 @@ CONFIGS = {
 STAGES = ("rows_prep_q", "rows_prep_k", "cols_prep_v", "scores_topk", "pv")
 
 
-def stage_bytes(c):
-    """Algorithmic HBM bytes each kernel must move per launch."""
+def stage_bytes(c, fused_pv):
+    """Algorithmic HBM bytes each kernel must move per launch.
+    fused_pv: the row kernel also does P.V (attn_rows2_kernel), so it reads the V
+    tables and writes the output, and there is no pv launch."""
     h = c["B"] * c["H"]
     N, T, D, k = c["N"], c["T"], c["D"], c["k"]
     nbd = -(-D // 32)
     dpad = 32 * nbd
     ntb = -(-T // 32)
     tpad = 32 * ntb
-    side = lambda rows: rows * (2 * dpad + 4 * nbd)  # codes + approx operand + 2 int16 exponents
-    return {
+    if c["mode"] == "ex_pred":  # codes + true/approx int16 exponents + sign words
+        side = lambda rows: rows * (dpad + 8 * nbd)
+    else:  # codes + approximator codes + 2 int16 exponents
+        side = lambda rows: rows * (2 * dpad + 4 * nbd)
+    vtab = D * tpad + 2 * ntb * D
+    by = {
         "rows_prep_q": h * (4 * N * D + side(N)),
         "rows_prep_k": h * (4 * T * D + side(T)),
-        "cols_prep_v": h * (4 * T * D + D * tpad + 2 * ntb * D),
-        "scores_topk": h * (side(N) + side(T) + 8 * N * k + N * tpad + 2 * N * ntb),
-        "pv": h * (N * tpad + 2 * N * ntb + D * tpad + 2 * ntb * D + 4 * N * D),
+        "cols_prep_v": h * (4 * T * D + vtab),
     }
+    if fused_pv:
+        by["scores_topk"] = h * (side(N) + side(T) + vtab + 8 * N * k + 4 * N * D)
+        by["pv"] = 0
+    else:
+        by["scores_topk"] = h * (side(N) + side(T) + 8 * N * k + N * tpad + 2 * N * ntb)
+        by["pv"] = h * (N * tpad + 2 * N * ntb + vtab + 4 * N * D)
+    return by
 
 
 def fused_min_bytes(c):
@@ -205,7 +216,8 @@ def main():
     tokens = world * c["B"] * c["N"] * args.steps
     value = tokens / elapsed
     stages = {s: float(stage_ms[i]) for i, s in enumerate(STAGES)}
-    by = stage_bytes(c)
+    fused_pv = stages["pv"] < 1e-3  # attn_rows2_kernel: P.V inside the row kernel
+    by = stage_bytes(c, fused_pv)
     dom = max(stages, key=stages.get)
     ach = by[dom] / (stages[dom] * 1e-3) / 1e9
     traffic = None
@@ -227,7 +239,7 @@ def main():
         "config": {"workload": c["workload"], "batch_per_gpu": c["B"], "heads": c["H"], "seq": c["N"],
                    "keys": c["T"], "head_dim": c["D"], "k": c["k"], "pred_mode": c["mode"],
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": "attn_rows2 (scores+top-k+softmax+P.V)" if fused_pv and dom == "scores_topk" else dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": by[dom], "mean_ms": stages[dom]},
         "stages_ms": stages,

@@ -15,7 +15,7 @@ import sys
 
 
 def stage_of(kernel):
-    if "attn_rows_kernel" in kernel or "scores_topk_kernel" in kernel:
+    if "attn_rows_kernel" in kernel or "attn_rows2_kernel" in kernel or "scores_topk_kernel" in kernel:
         return "scores_topk"
     if "rows_prep_kernel" in kernel:
         return "rows_prep"
