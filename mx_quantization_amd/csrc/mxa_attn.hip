@@ -620,6 +620,7 @@ struct TopkArgs {
   int n, k;
   int64_t* out_idx;
   float* out_vals;
+  int dbg;  // MXA_TOPK_DBG (tools only): 1 skip the lane tails, 2 skip the wave-wide steps
 };
 
 template <int S>
@@ -669,6 +670,89 @@ __global__ __launch_bounds__(256) void topk_reg_kernel(TopkArgs a) {
       }
     }
   }
+}
+
+// wave-wide steps while the pending range reaches past W, then one row per lane
+// (mxa_topk_lane.hpp).  A workgroup of WAVES waves takes 64 rows: the waves run
+// the wave-wide steps of the rows in turn and park each row's window [0, W) in a
+// shared pool; then the rows' lanes finish them (rows spread over TAILW waves).
+constexpr int kLaneRows = 64;  // rows per workgroup
+constexpr int kLaneStk = 16;   // lane stack entries (>= 2 lg W)
+template <int W>
+__host__ __device__ constexpr int lane_rs() { return W + 1; }  // u64 row stride (odd: spreads the banks)
+template <int S, int W, int WAVES>
+__host__ __device__ constexpr size_t topk_lane_lds() {
+  return (size_t)WAVES * topk_scratch_bytes(S) + (size_t)kLaneRows * (lane_rs<W>() * 8 + sizeof(LaneTask) + kLaneStk * 4);
+}
+
+template <int S, int W, int WAVES, int TAILW>
+__global__ __launch_bounds__(64 * WAVES) void topk_lane_kernel(TopkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int RS = lane_rs<W>();
+  unsigned char* wb = smem + (size_t)wave * topk_scratch_bytes(S);
+  unsigned char* pool = smem + (size_t)WAVES * topk_scratch_bytes(S);
+  lu64* stage = (lu64*)pool;                                                  // [64][RS]
+  LaneTask* tasks = reinterpret_cast<LaneTask*>(pool + kLaneRows * RS * 8);  // [64]
+  li32* stks = (li32*)(reinterpret_cast<int*>(tasks + kLaneRows));           // [64][kLaneStk]
+  const int64_t row0 = (int64_t)blockIdx.x * kLaneRows;
+  const int nrows = (int)min((int64_t)kLaneRows, a.rows - row0);
+  for (int r = wave; r < nrows; r += WAVES) {
+    RegTopk<S, false> tk;
+    tk.init(wb, a.n, lane);
+    const float* src = a.vals + (row0 + r) * a.ld;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      tk.K[s] = pos < a.n ? order_key(src[pos]) : 0u;
+      tk.I[s] = (uint32_t)pos;
+    }
+    LaneTask t;
+    if (a.dbg & 2) {
+      t.first = 0; t.last = min(a.n, W); t.depth = 2 * ilog2(a.n); t.nth = a.k - 1; t.k = a.k;
+    } else {
+      t = tk.select_big(a.k, W);
+    }
+    tk.stage_out(stage + r * RS, W);
+    if (lane == 0) tasks[r] = t;
+    wave_lds_sync();
+  }
+  __syncthreads();
+  {
+    // row r -> wave r % TAILW, lane r / TAILW
+    const int r = lane * TAILW + wave;
+    if (wave < TAILW && r < nrows && !(a.dbg & 1)) lane_topk_tail(stage + r * RS, tasks[r], stks + r * kLaneStk);
+  }
+  __syncthreads();
+  for (int r = wave; r < nrows; r += WAVES) {
+    if (lane < a.k) {
+      const uint32_t ix = (uint32_t)stage[r * RS + lane];
+      a.out_idx[(row0 + r) * a.k + lane] = (int64_t)ix;
+      if (a.out_vals) a.out_vals[(row0 + r) * a.k + lane] = a.vals[(row0 + r) * a.ld + ix];
+    }
+  }
+}
+
+template <int S, int W, int WAVES, int TAILW>
+static int launch_topk_lane(const TopkArgs& ta, hipStream_t stream) {
+  const size_t lds = topk_lane_lds<S, W, WAVES>();
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_lane_kernel<S, W, WAVES, TAILW>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const dim3 g((unsigned)((ta.rows + kLaneRows - 1) / kLaneRows));
+  hipLaunchKernelGGL((topk_lane_kernel<S, W, WAVES, TAILW>), g, dim3(64 * WAVES), lds, stream, ta);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int S, int W>
+static int launch_topk_lane_cfg(const TopkArgs& ta, hipStream_t stream) {
+  const char* env = getenv("MXA_LANE_CFG");  // tools only: WAVES x TAILW
+  const std::string c = env ? env : "8x8";
+  if (c == "4x1") return launch_topk_lane<S, W, 4, 1>(ta, stream);
+  if (c == "4x4") return launch_topk_lane<S, W, 4, 4>(ta, stream);
+  if (c == "8x1") return launch_topk_lane<S, W, 8, 1>(ta, stream);
+  if (c == "8x2") return launch_topk_lane<S, W, 8, 2>(ta, stream);
+  if (c == "16x16") return launch_topk_lane<S, W, 16, 16>(ta, stream);
+  return launch_topk_lane<S, W, 8, 8>(ta, stream);
 }
 
 // previous register-resident form (mxa_topk.hpp), kept for A/B timing (MXA_TOPK_V1)
@@ -1049,6 +1133,9 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     r2.bs0 = p->bias_strides[0]; r2.bs1 = p->bias_strides[1]; r2.bs2 = p->bias_strides[2]; r2.bs3 = p->bias_strides[3];
     r2.out = p->out; r2.os0 = p->out_strides[0]; r2.os1 = p->out_strides[1]; r2.os2 = p->out_strides[2];
     r2.idx_out = p->idx_out; r2.true_out = p->true_out; r2.pred_out = p->pred_out;
+#ifdef MXA_PHASE_PROF
+    r2.dbg = getenv("MXA_DBG_SKIP") ? atoi(getenv("MXA_DBG_SKIP")) : 0;
+#endif
     rc = launch_rows2(r2, rows_mode, p->top_k != 0, rows_S, (int)BH, stream);
     if (rc) return rc;
     if (ev) {
@@ -1124,7 +1211,9 @@ static int launch_topk(const TopkArgs& ta, hipStream_t stream) {
     hipLaunchKernelGGL(topk_rows_v1_kernel<S>, grid, dim3(256), (size_t)4 * (2 * 64 * S + kTopkStack / 2) * 8, stream, ta);
   else if (impl == "lds")
     hipLaunchKernelGGL(topk_rows_kernel<S>, grid, dim3(256), (size_t)4 * topk_scratch_bytes(S), stream, ta);
-  else
+  else if (impl != "reg" && ta.k <= 64) {  // lane-per-row tail
+    return ta.k <= 32 ? launch_topk_lane_cfg<S, 32>(ta, stream) : launch_topk_lane_cfg<S, 64>(ta, stream);
+  } else
     hipLaunchKernelGGL(topk_reg_kernel<S>, grid, dim3(256), (size_t)4 * topk_scratch_bytes(S), stream, ta);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
@@ -1134,7 +1223,8 @@ extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, 
   if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
   if (n > 512) return MXA_ERR_UNSUPPORTED;
   if (rows == 0 || k == 0) return MXA_OK;
-  TopkArgs ta{vals, rows, ld, n, k, out_idx, out_vals};
+  const char* dbg = getenv("MXA_TOPK_DBG");
+  TopkArgs ta{vals, rows, ld, n, k, out_idx, out_vals, dbg ? atoi(dbg) : 0};
   const int S = (n + 63) / 64;
   if (S <= 1) return launch_topk<1>(ta, stream);
   if (S <= 2) return launch_topk<2>(ta, stream);

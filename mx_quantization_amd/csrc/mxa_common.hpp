@@ -124,7 +124,20 @@ __device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int 
 
 // ---- wave64 helpers -------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+// wave-wide ballot straight from the compare mask (HIP's __ballot materialises the
+// predicate in a VGPR and compares it again)
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// bits [lo, hi) of a 64-bit lane mask, 0 <= lo <= hi <= 64 (uniform)
+__device__ __forceinline__ uint64_t range_mask64(int lo, int hi) {
+  const uint64_t h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  return lo >= 64 ? 0ull : h & ~((1ull << lo) - 1ull);
+}
+// set bits of m at or below this lane
+__device__ __forceinline__ int mbcnt_incl(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)__builtin_amdgcn_inverse_ballot_w64(m)));
+}
 __device__ __forceinline__ int mbcnt(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }

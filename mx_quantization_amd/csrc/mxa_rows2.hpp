@@ -46,7 +46,14 @@ struct Rows2Args {
   float* true_out;
   float* pred_out;
   int waves;  // waves per workgroup
+  int dbg;    // instrumented build only: phases to skip (tools/skip_prof.py), 0 otherwise
 };
+
+#ifdef MXA_PHASE_PROF
+#define MXA_SKIP2(bit) (a.dbg & (bit))
+#else
+#define MXA_SKIP2(bit) false
+#endif
 
 struct Rows2Lds {
   size_t mx, sT, op, sA, sg, vt, vs, waves, per_wave, total;
@@ -137,6 +144,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
   uint32_t* bm = reinterpret_cast<uint32_t*>(pe + 16);
 
   // ---- stage the head's K and V tables ---------------------------------------
+  MXA_PHASE_INIT();
   const int64_t kb = (int64_t)bh * T;
   {
     const int cpr = a.dpad / 16;
@@ -166,6 +174,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
     if (lane < 16) bm[lane] = 0u;
   }
   __syncthreads();
+  MXA_PHASE(0);
 
   for (int r = __builtin_amdgcn_readfirstlane(wave); r < a.N; r += a.waves) {
     const int64_t grow = (int64_t)bh * a.N + r;
@@ -175,7 +184,10 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
 
     // ---- the row's T values in position order ------------------------------
     float vals[S];
-    if constexpr (MODE == kModeExSign) {
+    if (MXA_SKIP2(4)) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) vals[s] = (float)((64 * s + lane) & 7);
+    } else if constexpr (MODE == kModeExSign) {
       // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
       uint32_t sq[kMaxNB];
       int eq[kMaxNB];
@@ -252,6 +264,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
 
     int ix[S];
     bool kept[S];
+    MXA_PHASE(1);
     if constexpr (TOPK) {
       // ---- top-k in torch's CPU order ----------------------------------------
       RegTopk<S, BIG> tk;
@@ -261,8 +274,11 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
         tk.K[s] = order_key(vals[s]);
         tk.I[s] = (uint32_t)(64 * s + lane);
       }
-      tk.run(a.k_top);
-      tk.finalize();
+      if (!MXA_SKIP2(1)) {
+        tk.run(a.k_top);
+        tk.finalize();
+      }
+      MXA_PHASE(2);
       // ---- vals = true.gather(idx); softmax ----------------------------------
       float v[S];
       float mx = -INFINITY;
@@ -277,7 +293,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
           if (kept[s]) {
             if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
             bool nan = false;
-            v[s] = true_of(ix[s], nan);
+            v[s] = MXA_SKIP2(8) ? (float)(ix[s] & 3) : true_of(ix[s], nan);
             mx = fmaxf(mx, v[s]);
           }
         }
@@ -290,6 +306,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
         sum += v[s];
       }
       sum = wave_sum_f32(sum);
+      MXA_PHASE(3);
       // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -360,8 +377,9 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
       wave_lds_sync();
     }
 
+    MXA_PHASE(4);
     // ---- out = MX(P) @ MX(V): v_dot4 over 16 keys per read, fp64 block epilogue
-    {
+    if (!MXA_SKIP2(2)) {
       double acc[2] = {0.0, 0.0};
       bool nan[2] = {false, false};
       const int dsl = D > 64 ? 2 : 1;
@@ -409,7 +427,9 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
         if (64 * s < a.k_top && pos < a.k_top) prow[ix[s]] = 0;
       }
     }
+    MXA_PHASE(5);
   }
+  MXA_PHASE_FLUSH();
 }
 
 }  // namespace mxa

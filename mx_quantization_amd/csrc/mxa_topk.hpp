@@ -127,8 +127,8 @@ struct WaveRow {
       if (s < s0 || s > s1) continue;  // uniform: slot outside the segment
       const uint64_t rr = range_mask(first - 64 * s, last - 64 * s);
       const uint64_t rl = range_mask(first + 1 - 64 * s, last - 64 * s);
-      L[s] = __ballot(key[s] <= p) & rl;  // left stop:  !(a > p)
-      R[s] = __ballot(key[s] >= p) & rr;  // right stop: !(p > a)
+      L[s] = ballot64(key[s] <= p) & rl;  // left stop:  !(a > p)
+      R[s] = ballot64(key[s] >= p) & rr;  // right stop: !(p > a)
       totL += __popcll(L[s]);
       totR += __popcll(R[s]);
     }
@@ -148,8 +148,8 @@ struct WaveRow {
       swl[s] = isl && Bgt > A;
       swr[s] = isr && A > Bgt;
       rank[s] = swl[s] ? A : Bgt;
-      SWL[s] = __ballot(swl[s]);
-      SWR[s] = __ballot(swr[s]);
+      SWL[s] = ballot64(swl[s]);
+      SWR[s] = ballot64(swr[s]);
       msw += __popcll(SWL[s]);
     }
     if (msw > 0) {  // exchange the t-th swapping left stop with the t-th swapping right stop

@@ -79,8 +79,8 @@ __device__ __forceinline__ int lds_partition(const TopkLdsV2& sc, int first, int
     const int rel = 64 * s + lane;
     const bool in = rel < len;
     const uint32_t k = key_of(v[s]);
-    Lb[s] = __ballot(in && rel > 0 && !(k > p));
-    Rb[s] = __ballot(in && !(p > k));
+    Lb[s] = ballot64(in && rel > 0 && !(k > p));
+    Rb[s] = ballot64(in && !(p > k));
     cl[s] = totL;
     cr[s] = totR;
     totL += __popcll(Lb[s]);
@@ -98,8 +98,8 @@ __device__ __forceinline__ int lds_partition(const TopkLdsV2& sc, int first, int
     swl[s] = isl && bgt > a;
     swr[s] = isr && a > bgt;
     rank[s] = swl[s] ? a : bgt;
-    SWL[s] = __ballot(swl[s]);
-    SWR[s] = __ballot(swr[s]);
+    SWL[s] = ballot64(swl[s]);
+    SWR[s] = ballot64(swr[s]);
     msw += __popcll(SWL[s]);
   }
   // the pivot swap is a real move even when the partition swaps nothing
@@ -236,11 +236,11 @@ __device__ __forceinline__ int win_partition(TopkWindow& win, int first, int las
   const bool in = pos >= first && pos < last;
   const bool isl = in && pos > first && !(k > p);
   const bool isr = in && !(p > k);
-  const uint64_t Lb = __ballot(isl), Rb = __ballot(isr);
+  const uint64_t Lb = ballot64(isl), Rb = ballot64(isr);
   const int a = (int)mbcnt(Lb);
   const int bgt = (int)__popcll(Rb) - (int)mbcnt(Rb) - (isr ? 1 : 0);
   const bool swl = isl && bgt > a, swr = isr && a > bgt;
-  const uint64_t SWL = __ballot(swl), SWR = __ballot(swr);
+  const uint64_t SWL = ballot64(swl), SWR = ballot64(swr);
   if (SWL) {  // exchange the t-th swapping left stop with the t-th swapping right stop
     const int rank = swl ? a : bgt;
     if (swl) sc.xa[rank] = v;
@@ -402,8 +402,8 @@ __device__ __forceinline__ void lds_sort_prefix_par(const TopkLdsV2& sc, int m, 
       const bool big = pos < m && l[s] - f[s] > 16;
       act[s] = big && d[s] > 0;
       heap[s] = big && d[s] == 0;
-      any_act |= __ballot(act[s]);
-      any_heap |= __ballot(heap[s]);
+      any_act |= ballot64(act[s]);
+      any_heap |= ballot64(heap[s]);
     }
     if (!any_act && !any_heap) break;
     if (any_heap) {  // std::__partial_sort(f, l, l) per exhausted segment, serial, one lane each
@@ -457,7 +457,7 @@ __device__ __forceinline__ void lds_sort_prefix_par(const TopkLdsV2& sc, int m, 
       const uint32_t k = key_of(v[s]);
       isl[s] = act[s] && pos > f[s] && !(k > p[s]);
       isr[s] = act[s] && !(p[s] > k);
-      const uint64_t Lb = __ballot(isl[s]), Rb = __ballot(isr[s]);
+      const uint64_t Lb = ballot64(isl[s]), Rb = ballot64(isr[s]);
       pl[s] = totL + (int)mbcnt(Lb);
       pr[s] = totR + (int)mbcnt(Rb);
       totL += (int)__popcll(Lb);
@@ -486,7 +486,7 @@ __device__ __forceinline__ void lds_sort_prefix_par(const TopkLdsV2& sc, int m, 
         swr[s] = isr[s] && a > bgt;
         xi[s] = f[s] / 2 + (swl[s] ? a : bgt);
       }
-      any_sw |= __ballot(swl[s] || swr[s]);
+      any_sw |= ballot64(swl[s] || swr[s]);
     }
     // the write of the swapped / pivot-moved values happens after the exchange
     if (any_sw) {

@@ -21,6 +21,7 @@
 //     (mxa_topk_lds.hpp), materialised only on those paths.
 #pragma once
 #include "mxa_topk_lds.hpp"
+#include "mxa_topk_lane.hpp"
 
 namespace mxa {
 
@@ -39,7 +40,9 @@ template <> struct SlotVec<8> { typedef uint32_t __attribute__((ext_vector_type(
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 // writelane: lane l takes the uniform value v (v_cmp + v_cndmask)
-__device__ __forceinline__ uint32_t wrl(uint32_t old, uint32_t v, int l) { return lane_id() == l ? v : old; }
+__device__ __forceinline__ uint32_t wrl(uint32_t old, uint32_t v, int l) {
+  return __builtin_amdgcn_inverse_ballot_w64(1ull << l) ? v : old;
+}
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 
 // __move_median_to_first(first, a = first+1, b = mid, c = last-1) with cmp = greater:
@@ -114,15 +117,17 @@ __device__ __forceinline__ int win_step(RWin& w, int f, int l, lds_u64* X, int h
     w.k = wrl(w.k, kf, rm);
     w.i = wrl(w.i, jf, rm);
   }
-  const bool inr = lane >= rf && lane < rl;
-  const bool isl = inr && lane != rf && !(w.k > p);  // left stop in [first+1, last)
-  const bool isr = inr && !(p > w.k);                // right stop in [first, last)
-  const uint64_t Lb = __ballot(isl), Rb = __ballot(isr);
-  const int a = mbcnt(Lb);                                              // left stops below
-  const int u = (int)__popcll(Rb) - mbcnt(Rb) - (isr ? 1 : 0);          // right stops above
-  const bool swl = isl && u > a, swr = isr && a > u;
-  const uint64_t SWL = __ballot(swl), SWR = __ballot(swr);
-  if (SWL) exchange(w.k, w.i, swl, swr, swl ? a : u, X, half);
+  // stops as lane masks: compares straight to SGPRs, the range by SALU
+  const uint64_t rng = range_mask64(rf, rl);
+  const uint64_t Lb = ballot64(!(w.k > p)) & rng & ~(1ull << rf);  // left stops in [first+1, last)
+  const uint64_t Rb = ballot64(!(p > w.k)) & rng;                   // right stops in [first, last)
+  const int a = mbcnt(Lb);                                          // left stops below
+  const int u = (int)__popcll(Rb) - mbcnt_incl(Rb);                 // right stops above
+  const uint64_t SWL = ballot64(u > a) & Lb, SWR = ballot64(a > u) & Rb;
+  if (SWL) {
+    const bool swl = __builtin_amdgcn_inverse_ballot_w64(SWL);
+    exchange(w.k, w.i, swl, __builtin_amdgcn_inverse_ballot_w64(SWR), swl ? a : u, X, half);
+  }
   // cut = min(first non-swapping left stop, lowest swapping right stop | last)
   const uint64_t nsl = Lb & ~SWL;
   const int c1 = nsl ? ffs64(nsl) : 1 << 20;
@@ -144,47 +149,44 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
     uset(K, m, kf);
     uset(I, m, jf);
   }
+  // stops as lane masks: single compares straight to SGPRs, combined by SALU
   uint64_t Lb[S], Rb[S];
-  bool isl[S], isr[S];
   int cl[S], cr[S];
   int totL = 0, totR = 0;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int pos = 64 * s + lane;
-    const bool inr = pos >= f && pos < l;
-    isl[s] = inr && pos != f && !(K[s] > p);
-    isr[s] = inr && !(p > K[s]);
-    Lb[s] = __ballot(isl[s]);
-    Rb[s] = __ballot(isr[s]);
+    const uint64_t inr = ballot64(pos >= f) & ballot64(pos < l);
+    Lb[s] = inr & ballot64(!(K[s] > p)) & ~ballot64(pos == f);  // left stops in [first+1, last)
+    Rb[s] = inr & ballot64(!(p > K[s]));                         // right stops in [first, last)
     cl[s] = totL;
     cr[s] = totR;
     totL += (int)__popcll(Lb[s]);
     totR += (int)__popcll(Rb[s]);
   }
-  bool swl[S], swr[S];
   int rank[S];
   uint64_t SWL[S], SWR[S];
   uint64_t anysw = 0ull;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int a = cl[s] + mbcnt(Lb[s]);
-    const int u = totR - cr[s] - mbcnt(Rb[s]) - (isr[s] ? 1 : 0);
-    swl[s] = isl[s] && u > a;
-    swr[s] = isr[s] && a > u;
-    rank[s] = swl[s] ? a : u;
-    SWL[s] = __ballot(swl[s]);
-    SWR[s] = __ballot(swr[s]);
+    const int a = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Lb[s] >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)Lb[s], (uint32_t)cl[s]));
+    const int u = totR - cr[s] - mbcnt_incl(Rb[s]);
+    SWL[s] = ballot64(u > a) & Lb[s];
+    SWR[s] = ballot64(a > u) & Rb[s];
+    rank[s] = __builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? a : u;
     anysw |= SWL[s];
   }
   if (anysw) {
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      if (swl[s] || swr[s]) X[swl[s] ? rank[s] : half + rank[s]] = pack_ki(K[s], I[s]);
+      if (__builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s]))
+        X[__builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? rank[s] : half + rank[s]] = pack_ki(K[s], I[s]);
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (swl[s] || swr[s]) {
-        const uint64_t v = X[swl[s] ? half + rank[s] : rank[s]];
+      if (__builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s])) {
+        const uint64_t v = X[__builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? half + rank[s] : rank[s]];
         K[s] = (uint32_t)(v >> 32);
         I[s] = (uint32_t)v;
       }
@@ -352,6 +354,76 @@ struct RegTopk {
       small_insertion(first, last);
     }
     return false;
+  }
+
+  // The wave-wide part of run(k) when the lanes finish the row (mxa_topk_lane.hpp):
+  // __introselect steps only while the pending range reaches past position W
+  // (k <= W <= 64).  Returns the hand-off state; first == last when selection is
+  // complete (depth-limit fallback, a final <= 3 range past W, or partial_sort,
+  // which also leaves the prefix sorted: then k = 0 in the task).
+  __device__ __forceinline__ LaneTask select_big(int k, int W) {
+    const int half = 32 * S;
+    LaneTask t;
+    t.nth = k - 1;
+    t.k = k;
+    t.first = t.last = t.depth = 0;
+    if (k * 64 <= n) {  // std::partial_sort(begin, begin+k, end)
+      to_lds();
+      if (lane == 0) {
+        s_heap_select(sc().A, 0, k, n);
+        s_sort_heap(sc().A, 0, k);
+      }
+      wave_lds_sync();
+      t.k = 0;
+      return t;
+    }
+    int first = 0, last = n;
+    const int nth = k - 1;
+    int depth = 2 * ilog2(n);
+    while (last - first > 3 && last > W) {
+      if (depth == 0) {  // std::__heap_select(first, nth+1, last); iter_swap(first, nth)
+        to_lds();
+        if (lane == 0) {
+          s_heap_select(sc().A, first, nth + 1, last);
+          const uint64_t x = A[first];
+          A[first] = A[nth];
+          A[nth] = x;
+        }
+        wave_lds_sync();
+        return t;
+      }
+      --depth;
+      int cut;
+      if (mode == kWin || last - first <= 64) {
+        if (mode != kWin) to_win(win_base(first));
+        cut = win_step(w, first, last, X, half, lane);
+      } else {
+        cut = slots_step<S>(K, I, first, last, X, half, lane);
+      }
+      if (cut <= nth) first = cut;
+      else last = cut;
+    }
+    if (last > W) {  // a final <= 3 range that reaches past W: __insertion_sort here
+      if (last - first > 1) {
+        if (mode != kWin) to_win(win_base(first));
+        small_insertion(first, last);
+      }
+      return t;
+    }
+    t.first = first;
+    t.last = last;
+    t.depth = depth;
+    return t;
+  }
+
+  // positions [0, W) of the row to dst[0, W) (W <= 64)
+  __device__ __forceinline__ void stage_out(lu64* dst, int W) {
+    if (mode == kWin && w.b != 0) to_lds();
+    uint64_t v;
+    if (mode == kSlots) v = pack_ki(K[0], I[0]);
+    else if (mode == kWin) v = pack_ki(w.k, w.i);
+    else v = A[lane];
+    if (lane < W) dst[lane] = v;
   }
 
   // std::sort(begin, begin + m) for m <= 64 on the window at base 0:

@@ -110,9 +110,9 @@ def test_exponent_rule_exhaustive_sample(M):
 
 
 # ------------------------------------------------------------------ top-k order
-@pytest.fixture(params=["reg", "lds"])
+@pytest.fixture(params=["lane", "reg", "lds"])
 def impl(request):
-    """standalone top-k on the register-resident (default) and LDS-resident rows"""
+    """standalone top-k: lane-per-row tail (default for k <= 64), register-resident and LDS-resident rows"""
     os.environ["MXA_TOPK_IMPL"] = request.param
     yield request.param
     os.environ.pop("MXA_TOPK_IMPL", None)
@@ -156,6 +156,18 @@ def test_topk_random_small_alphabets_and_specials(M, impl):
             _, want = O.topk(rows, k)
             _, idx = M.topk(dev(rows), k)
             same(host(idx), want, f"n{n} k{k}")
+
+
+@pytest.mark.parametrize("n", [33, 64, 65, 100, 197, 256, 512])
+def test_topk_lane_tail_many_rows(M, n):
+    """the lane-per-row tail (windows W = 32 and 64) on thousands of rows with heavy ties"""
+    rng = np.random.default_rng(n)
+    for k in sorted({1, 2, 5, 16, 17, 20, 30, 32, 33, 48, 64} & set(range(1, n + 1))):
+        rows = rng.integers(-6, 7, (700, n)).astype(np.float32) * np.float32(0.25)
+        rows[:100] = rng.standard_normal((100, n)).astype(np.float32)
+        _, want = O.topk(rows, k)
+        _, idx = M.topk(dev(rows), k)
+        same(host(idx), want, f"n{n} k{k}")
 
 
 # ------------------------------------------------------------------ approximators

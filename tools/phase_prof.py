@@ -15,7 +15,7 @@ from mx_quantization_amd import _native as N
 
 fn = N.lib().mxa_debug_phase_cycles
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-names = ["stage", "scores", "select", "sort", "gather+softmax", "P quant+store"]
+names = ["stage", "scores", "topk", "gather+softmax", "P quant", "PV+store"]
 skips = [int(x) for x in os.environ.get("PHASE_SKIPS", "0").split(",")]
 for cfg, (B, H, Nq, D, k) in {"deit_base": (256, 12, 197, 64, 20), "dit_xl2": (64, 16, 256, 72, 154)}.items():
     q, kk, v = (torch.from_numpy(np.random.default_rng(s).standard_normal((B, H, Nq, D), dtype=np.float32)).cuda()

@@ -30,7 +30,7 @@ for cfg in sys.argv[1].split(",") if len(sys.argv) > 1 else cfgs:
     out, idx, t, p = M.mx_topk_attention(q, kk, v, D ** -0.5, k_top=k, return_scores=True)
     rows = p.reshape(-1, N).contiguous()
     res = {}
-    for impl in ("reg", "lds"):
+    for impl in ("lane", "reg", "lds"):
         os.environ["MXA_TOPK_IMPL"] = impl
         res["topk_" + impl] = timeit(lambda: M.topk(rows, k))
     os.environ.pop("MXA_TOPK_IMPL")
