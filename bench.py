@@ -51,35 +51,38 @@ CONFIGS = {
     "pixart_cross": dict(workload="PixArt-alpha 256x256 cross-attention core, MXINT4 (Sanger) approximator",
                          B=8, H=16, N=256, T=120, D=72, k=20, mode="MXINT4", scale=1 / np.sqrt(72), bias=True),
 }
-STAGES = ("rows_prep_q", "rows_prep_k", "cols_prep_v", "scores_topk", "pv")
+STAGES = ("rows_prep_q", "rows_prep_k", "cols_prep_v", "row kernel(s)", "")  # names: stage_bytes()
 
 
-def stage_bytes(c, fused_pv):
-    """Algorithmic HBM bytes each kernel must move per launch.
-    fused_pv: the row kernel also does P.V (attn_rows2_kernel), so it reads the V
-    tables and writes the output, and there is no pv launch."""
+def stage_bytes(c, path):
+    """Algorithmic HBM bytes each kernel must move per launch, by the
+    kernel path mxa_attention_path() reports:
+      rows_split  stage 3 = selection kernel (scores + top-k; writes the kept indices),
+                  stage 4 = finishing kernel (gather, softmax, P, P.V; writes out)
+      rows_fused  stage 3 = the one row kernel, stage 4 empty"""
     h = c["B"] * c["H"]
     N, T, D, k = c["N"], c["T"], c["D"], c["k"]
     nbd = -(-D // 32)
     dpad = 32 * nbd
     ntb = -(-T // 32)
     tpad = 32 * ntb
-    if c["mode"] == "ex_pred":  # codes + true/approx int16 exponents + sign words
-        side = lambda rows: rows * (dpad + 8 * nbd)
-    else:  # codes + approximator codes + 2 int16 exponents
-        side = lambda rows: rows * (2 * dpad + 4 * nbd)
+    codes = lambda rows: rows * (dpad + 2 * nbd)  # MXINT8 codes + int16 block exponents
+    if c["mode"] == "ex_pred":  # sign words + int16 block exponents
+        apx = lambda rows: rows * (4 * nbd + 2 * nbd)
+    else:  # approximator codes + int16 block scales
+        apx = lambda rows: rows * (dpad + 2 * nbd)
     vtab = D * tpad + 2 * ntb * D
     by = {
-        "rows_prep_q": h * (4 * N * D + side(N)),
-        "rows_prep_k": h * (4 * T * D + side(T)),
+        "rows_prep_q": h * (4 * N * D + codes(N) + apx(N)),
+        "rows_prep_k": h * (4 * T * D + codes(T) + apx(T)),
         "cols_prep_v": h * (4 * T * D + vtab),
     }
-    if fused_pv:
-        by["scores_topk"] = h * (side(N) + side(T) + vtab + 8 * N * k + 4 * N * D)
-        by["pv"] = 0
+    if path == "rows_split":
+        by["select"] = h * (apx(N) + apx(T) + 8 * N * k + 4 * N * k)
+        by["finish"] = h * (codes(N) + codes(T) + vtab + 4 * N * k + 4 * N * D)
     else:
-        by["scores_topk"] = h * (side(N) + side(T) + 8 * N * k + N * tpad + 2 * N * ntb)
-        by["pv"] = h * (N * tpad + 2 * N * ntb + vtab + 4 * N * D)
+        by["fused"] = h * (codes(N) + codes(T) + apx(N) + apx(T) + vtab + 8 * N * k + 4 * N * D)
+        by["-"] = 0
     return by
 
 
@@ -215,9 +218,10 @@ def main():
 
     tokens = world * c["B"] * c["N"] * args.steps
     value = tokens / elapsed
-    stages = {s: float(stage_ms[i]) for i, s in enumerate(STAGES)}
-    fused_pv = stages["pv"] < 1e-3  # attn_rows2_kernel: P.V inside the row kernel
-    by = stage_bytes(c, fused_pv)
+    path = N.PATH_NAMES.get(N.lib().mxa_attention_path(ctypes.byref(p)), "?")
+    by = stage_bytes(c, path)
+    names = list(by)  # stage order of mxa_attention_timed
+    stages = {names[i]: float(stage_ms[i]) for i in range(len(STAGES))}
     dom = max(stages, key=stages.get)
     ach = by[dom] / (stages[dom] * 1e-3) / 1e9
     traffic = None
@@ -239,7 +243,7 @@ def main():
         "config": {"workload": c["workload"], "batch_per_gpu": c["B"], "heads": c["H"], "seq": c["N"],
                    "keys": c["T"], "head_dim": c["D"], "k": c["k"], "pred_mode": c["mode"],
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "attn_rows2 (scores+top-k+softmax+P.V)" if fused_pv and dom == "scores_topk" else dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": dom, "path": path, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": by[dom], "mean_ms": stages[dom]},
         "stages_ms": stages,

@@ -149,10 +149,25 @@ int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p);
 int mxa_attention(const mxa_attn_params* p, hipStream_t stream);
 
 /*
+ * Which kernels mxa_attention(p) runs (no launch; the workspace may be null):
+ *   MXA_PATH_ROWS_SPLIT  selection kernel (scores + top-k) then finishing kernel
+ *                        (gather, softmax, P, P.V) -- the default for top-k
+ *   MXA_PATH_ROWS_FUSED  one row kernel for all of it (dense softmax, or MXA_ATTN_PATH=fused)
+ *   MXA_PATH_ROWS_V1 / MXA_PATH_TILES  earlier layouts, kept for large heads
+ * or a negative MXA_ERR_* for invalid parameters.
+ */
+#define MXA_PATH_TILES 0
+#define MXA_PATH_ROWS_V1 1
+#define MXA_PATH_ROWS_FUSED 2
+#define MXA_PATH_ROWS_SPLIT 3
+int mxa_attention_path(const mxa_attn_params* p);
+
+/*
  * Measurement entry point (bench.py): runs mxa_attention `iters` times on `stream`
  * recording HIP events between the kernels, synchronizes the stream, and writes
  * the mean milliseconds of each stage to stage_ms[MXA_ATTN_STAGES]:
- *   0 rows_prep(Q)  1 rows_prep(K)  2 cols_prep(V)  3 scores+top-k+softmax+P-quant  4 P.V
+ *   0 rows_prep(Q)  1 rows_prep(K)  2 cols_prep(V)  3 scores+top-k (the whole fused row kernel
+ *   on MXA_PATH_ROWS_FUSED)  4 gather+softmax+P+P.V (0 on MXA_PATH_ROWS_FUSED)
  * Host-synchronizing: not for use inside graph capture.
  */
 #define MXA_ATTN_STAGES 5

@@ -21,6 +21,7 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
+PATH_NAMES = {0: "tiles", 1: "rows_v1", 2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
 PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4}
 ROUND_MODES = {"nearest": 0, "floor": 1, "even": 2}
 
@@ -51,6 +52,7 @@ _SIGS = {
     "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "mxa_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams)]),
     "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
+    "mxa_attention_path": (c_i32, [ctypes.POINTER(AttnParams)]),
     "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                            c_vp, c_i64, c_vp]),

@@ -225,7 +225,7 @@ __device__ unsigned long long g_phase_cycles[16];
 // per-wave sums in registers, flushed once per wave (MXA_PHASE_FLUSH)
 #define MXA_PHASE_INIT() \
   uint64_t ph_t = clock64(); \
-  uint64_t ph_acc[6] = {0, 0, 0, 0, 0, 0}
+  uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define MXA_PHASE(i)                  \
   do {                                \
     const uint64_t ph_n = clock64();  \
@@ -235,7 +235,7 @@ __device__ unsigned long long g_phase_cycles[16];
 #define MXA_PHASE_FLUSH()                                                   \
   do {                                                                      \
     if (lane == 0)                                                          \
-      for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase_cycles[i_], ph_acc[i_]); \
+      for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phase_cycles[i_], ph_acc[i_]); \
   } while (0)
 #else
 #define MXA_PHASE_INIT() (void)0
@@ -844,7 +844,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qsT, qsA, qsg, kc, kop, ksT, ksA, ksg, vt, vs, pc, ps, total;
+  int64_t qc, qop, qsT, qsA, qsg, kc, kop, ksT, ksA, ksg, vt, vs, pc, ps, idx32, total;
 };
 
 AttnLayout attn_layout(const mxa_attn_params* p) {
@@ -875,6 +875,7 @@ AttnLayout attn_layout(const mxa_attn_params* p) {
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
   L.pc = take(qrows * L.tpad);
   L.ps = take(qrows * L.ntb * 2);
+  L.idx32 = take(p->top_k ? qrows * (int64_t)p->k_top * 4 : 0);
   L.total = off;
   return L;
 }
@@ -958,66 +959,95 @@ static int launch_rows(const RowsArgs& ra, int mode, int S, int BH, hipStream_t 
   }
 }
 
-// ---- fused row kernel v2 (mxa_rows2.hpp) -----------------------------------
-static size_t rows2_total(int mode, bool topk, const Rows2Args& ra, int S, int W) {
-  return rows2_lds(mode, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, S, ra.tpad, topk ? ra.k_top : 0, W).total;
+// ---- row kernels v2 (mxa_rows2.hpp): fused (part 0) or split (parts 1 + 2) ----
+static size_t rows2_total(int mode, bool topk, const Rows2Args& ra, int S, int W, int part) {
+  return rows2_lds(mode, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, S, ra.tpad, topk ? ra.k_top : 0, W, part).total;
 }
-// waves per workgroup: two 8-wave workgroups per CU when they fit, else one 16-wave one
-static int rows2_waves(int mode, bool topk, const Rows2Args& ra, int S) {
-  const char* env = getenv("MXA_ROWS2_WAVES");
+// waves per workgroup.  Fused / finishing kernel: two 8-wave workgroups per CU when
+// they fit, else one 16-wave one.  Selection kernel: 4-wave workgroups (its LDS is
+// the small score tables and the per-wave top-k scratch), as many per CU as fit.
+static int rows2_waves(int mode, bool topk, const Rows2Args& ra, int S, int part) {
+  const char* env = getenv(part == 1 ? "MXA_SELECT_WAVES" : "MXA_ROWS2_WAVES");
   if (env) {
     const int w = atoi(env);
-    return rows2_total(mode, topk, ra, S, w) <= 160 * 1024 ? w : 0;
+    const int wmax = part == 1 ? 4 : 16;
+    return w <= wmax && rows2_total(mode, topk, ra, S, w, part) <= 160 * 1024 ? w : 0;
   }
-  if (rows2_total(mode, topk, ra, S, 8) <= 80 * 1024) return 8;
-  if (rows2_total(mode, topk, ra, S, 16) <= 160 * 1024) return 16;
-  if (rows2_total(mode, topk, ra, S, 8) <= 160 * 1024) return 8;
-  if (rows2_total(mode, topk, ra, S, 4) <= 160 * 1024) return 4;
+  if (part == 1) return rows2_total(mode, topk, ra, S, 4, part) <= 160 * 1024 ? 4 : 0;
+  if (rows2_total(mode, topk, ra, S, 8, part) <= 80 * 1024) return 8;
+  if (rows2_total(mode, topk, ra, S, 16, part) <= 160 * 1024) return 16;
+  if (rows2_total(mode, topk, ra, S, 8, part) <= 160 * 1024) return 8;
+  if (rows2_total(mode, topk, ra, S, 4, part) <= 160 * 1024) return 4;
   return 0;
 }
 
-template <int S, int MODE, bool TOPK, bool BIG>
-static int launch_rows2_b(const Rows2Args& ra0, int BH, hipStream_t stream) {
+template <int S, int MODE, bool TOPK, bool BIG, int PART>
+static int launch_rows2_p(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
-  ra.waves = rows2_waves(MODE, TOPK, ra, S);
+  ra.waves = rows2_waves(MODE, TOPK, ra, S, PART);
   if (ra.waves <= 0) return MXA_ERR_UNSUPPORTED;
-  const size_t lds = rows2_total(MODE, TOPK, ra, S, ra.waves);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows2_kernel<S, MODE, TOPK, BIG>),
+  const size_t lds = rows2_total(MODE, TOPK, ra, S, ra.waves, PART);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows2_kernel<S, MODE, TOPK, BIG, PART>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL((attn_rows2_kernel<S, MODE, TOPK, BIG>), dim3((unsigned)BH), dim3(64 * ra.waves), lds, stream,
-                     ra);
+  // few heads (PixArt cross-attention: 128): split each head's rows over grid.y so
+  // that the launch still has ~4 workgroups per CU
+  const int chunks = std::max(1, std::min((ra.N + ra.waves - 1) / ra.waves, 1024 / std::max(BH, 1)));
+  ra.rows_per_wg = (ra.N + chunks - 1) / chunks;
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL((attn_rows2_kernel<S, MODE, TOPK, BIG, PART>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds,
+                     stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+// split: the selection kernel, an event, the finishing kernel
+template <int S, int MODE, bool TOPK, bool BIG>
+static int launch_rows2_b(const Rows2Args& ra, int BH, bool split, hipStream_t stream, hipEvent_t* ev) {
+  int rc;
+  if (TOPK && split) {
+    rc = launch_rows2_p<S, MODE, TOPK, BIG, 1>(ra, BH, stream);
+    if (rc) return rc;
+    if (ev) (void)hipEventRecord(ev[4], stream);
+    rc = launch_rows2_p<S, MODE, TOPK, BIG, 2>(ra, BH, stream);
+  } else {
+    rc = launch_rows2_p<S, MODE, TOPK, BIG, 0>(ra, BH, stream);
+    if (ev) (void)hipEventRecord(ev[4], stream);
+  }
+  if (!rc && ev) (void)hipEventRecord(ev[5], stream);
+  return rc;
 }
 
 // BIG: a sorted prefix longer than 64 is possible (k > 65)
 template <int S, int MODE, bool TOPK>
-static int launch_rows2_s(const Rows2Args& ra, int BH, hipStream_t stream) {
-  if (TOPK && ra.k_top > 65) return launch_rows2_b<S, MODE, TOPK, true>(ra, BH, stream);
-  return launch_rows2_b<S, MODE, TOPK, false>(ra, BH, stream);
+static int launch_rows2_s(const Rows2Args& ra, int BH, bool split, hipStream_t stream, hipEvent_t* ev) {
+  if (TOPK && ra.k_top > 65) return launch_rows2_b<S, MODE, TOPK, true>(ra, BH, split, stream, ev);
+  return launch_rows2_b<S, MODE, TOPK, false>(ra, BH, split, stream, ev);
 }
 
 template <int S>
-static int launch_rows2_mode(const Rows2Args& ra, int mode, bool topk, int BH, hipStream_t stream) {
-  if (!topk) return launch_rows2_s<S, kModeTrue, false>(ra, BH, stream);
+static int launch_rows2_mode(const Rows2Args& ra, int mode, bool topk, int BH, bool split, hipStream_t stream,
+                             hipEvent_t* ev) {
+  if (!topk) return launch_rows2_s<S, kModeTrue, false>(ra, BH, false, stream, ev);
   switch (mode) {
-    case kModeOpExp: return launch_rows2_s<S, kModeOpExp, true>(ra, BH, stream);
-    case kModeOpMul: return launch_rows2_s<S, kModeOpMul, true>(ra, BH, stream);
-    case kModeExSign: return launch_rows2_s<S, kModeExSign, true>(ra, BH, stream);
-    default: return launch_rows2_s<S, kModeTrue, true>(ra, BH, stream);
+    case kModeOpExp: return launch_rows2_s<S, kModeOpExp, true>(ra, BH, split, stream, ev);
+    case kModeOpMul: return launch_rows2_s<S, kModeOpMul, true>(ra, BH, split, stream, ev);
+    case kModeExSign: return launch_rows2_s<S, kModeExSign, true>(ra, BH, split, stream, ev);
+    default: return launch_rows2_s<S, kModeTrue, true>(ra, BH, split, stream, ev);
   }
 }
 
-static int launch_rows2(const Rows2Args& ra, int mode, bool topk, int S, int BH, hipStream_t stream) {
+static int launch_rows2(const Rows2Args& ra, int mode, bool topk, int S, int BH, bool split, hipStream_t stream,
+                        hipEvent_t* ev) {
   switch (S) {
-    case 1: return launch_rows2_mode<1>(ra, mode, topk, BH, stream);
-    case 2: return launch_rows2_mode<2>(ra, mode, topk, BH, stream);
-    case 4: return launch_rows2_mode<4>(ra, mode, topk, BH, stream);
-    default: return launch_rows2_mode<8>(ra, mode, topk, BH, stream);
+    case 1: return launch_rows2_mode<1>(ra, mode, topk, BH, split, stream, ev);
+    case 2: return launch_rows2_mode<2>(ra, mode, topk, BH, split, stream, ev);
+    case 4: return launch_rows2_mode<4>(ra, mode, topk, BH, split, stream, ev);
+    default: return launch_rows2_mode<8>(ra, mode, topk, BH, split, stream, ev);
   }
 }
 
-static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev) {
+// plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing
+static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr) {
   if (!p || !p->q || !p->k || !p->v || !p->out) return MXA_ERR_ARG;
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
   if (p->T > 512) return MXA_ERR_UNSUPPORTED;
@@ -1025,9 +1055,6 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   if (p->pred_mode < MXA_PRED_EX_PRED || p->pred_mode > MXA_PRED_EXION) return MXA_ERR_ARG;
   if (p->bfloat != 0 && p->bfloat != 32 && (p->bfloat < 10 || p->bfloat > 31)) return MXA_ERR_ARG;
   const AttnLayout L = attn_layout(p);
-  if (!p->workspace || p->workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
-  unsigned char* ws = static_cast<unsigned char*>(p->workspace);
-  if (!aligned16(ws)) return MXA_ERR_ARG;
   const int64_t BH = (int64_t)p->B * p->H;
 
   int opq = MXA_OP_SIGN, opk = MXA_OP_SIGN;
@@ -1053,11 +1080,21 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.T = p->T; r2.D = p->D; r2.nbd = L.nbd; r2.ntb = L.ntb; r2.tpad = L.tpad; r2.k_top = p->k_top;
   r2.kst = kst; r2.vst = L.tpad + 16;
   const bool rows2_path = L.nbd <= kMaxNB && path != "tiles" && path != "rows1" &&
-                          rows2_waves(rows_mode, p->top_k != 0, r2, rows_S) > 0;
+                          rows2_waves(rows_mode, p->top_k != 0, r2, rows_S, 0) > 0;
+  // split (default for top-k): selection kernel + finishing kernel; "fused": one kernel
+  const bool split = p->top_k && path != "fused" && rows2_waves(rows_mode, true, r2, rows_S, 1) > 0 &&
+                     rows2_waves(rows_mode, true, r2, rows_S, 2) > 0;
   const bool rows_path = rows2_path ||
                          (L.nbd <= kMaxNB &&
                           rows_lds(rows_mode, p->T, kst, L.nbd, rows_S, L.tpad, p->top_k != 0).total <= 160 * 1024 &&
                           path != "tiles");
+  if (plan) {
+    *plan = rows2_path ? (split ? MXA_PATH_ROWS_SPLIT : MXA_PATH_ROWS_FUSED) : rows_path ? MXA_PATH_ROWS_V1 : MXA_PATH_TILES;
+    return MXA_OK;
+  }
+  if (!p->workspace || p->workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
+  unsigned char* ws = static_cast<unsigned char*>(p->workspace);
+  if (!aligned16(ws)) return MXA_ERR_ARG;
   // the ex_pred rows kernel derives the sign operand from the MX codes
   const bool need_op = need_pred && !(rows_path && rows_mode == kModeExSign);
 
@@ -1136,13 +1173,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
 #ifdef MXA_PHASE_PROF
     r2.dbg = getenv("MXA_DBG_SKIP") ? atoi(getenv("MXA_DBG_SKIP")) : 0;
 #endif
-    rc = launch_rows2(r2, rows_mode, p->top_k != 0, rows_S, (int)BH, stream);
-    if (rc) return rc;
-    if (ev) {
-      (void)hipEventRecord(ev[4], stream);
-      (void)hipEventRecord(ev[5], stream);
-    }
-    return MXA_OK;
+    r2.idx32 = reinterpret_cast<int32_t*>(ws + L.idx32);
+    return launch_rows2(r2, rows_mode, p->top_k != 0, rows_S, (int)BH, split, stream, ev);
   } else if (rows_path) {
     RowsArgs ra{};
     ra.s = sa;
@@ -1177,6 +1209,12 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
 
 extern "C" int mxa_attention(const mxa_attn_params* p, hipStream_t stream) {
   return attention_impl(p, stream, nullptr);
+}
+
+extern "C" int mxa_attention_path(const mxa_attn_params* p) {
+  int plan = -1;
+  const int rc = attention_impl(p, nullptr, nullptr, &plan);
+  return rc ? rc : plan;
 }
 
 extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms) {

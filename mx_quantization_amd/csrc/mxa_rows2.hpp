@@ -45,7 +45,9 @@ struct Rows2Args {
   int64_t* idx_out;
   float* true_out;
   float* pred_out;
-  int waves;  // waves per workgroup
+  int waves;        // waves per workgroup
+  int rows_per_wg;  // query rows per workgroup (grid.y splits a head when there are few heads)
+  int32_t* idx32;  // split path: the kept indices [B*H*N][k_top] between the two kernels
   int dbg;    // instrumented build only: phases to skip (tools/skip_prof.py), 0 otherwise
 };
 
@@ -61,28 +63,33 @@ struct Rows2Lds {
 
 __host__ __device__ inline size_t r2_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// part: 0 the fused kernel; 1 the selection kernel (scores + top-k, writes the
+// kept indices); 2 the finishing kernel (gather, softmax, P, P.V from the indices)
 __host__ __device__ inline Rows2Lds rows2_lds(int mode, int T, int D, int kst, int nbd, int vst, int ntb, int S,
-                                              int tpad, int k_top, int waves) {
+                                              int tpad, int k_top, int waves, int part = 0) {
   Rows2Lds L;
   size_t o = 0;
+  const bool codes = part != 1 || mode == kModeTrue;  // true scores: the top-k values or the gather
+  const bool apx = part != 2;                         // approximate scores
   L.mx = o;
-  o += r2_al16((size_t)T * kst);
+  if (codes) o += r2_al16((size_t)T * kst);
   L.sT = o;
-  o += r2_al16((size_t)T * nbd * 2);
+  if (codes) o += r2_al16((size_t)T * nbd * 2);
   L.op = o;
-  if (mode == kModeOpExp || mode == kModeOpMul) o += r2_al16((size_t)T * kst);
+  if (apx && (mode == kModeOpExp || mode == kModeOpMul)) o += r2_al16((size_t)T * kst);
   L.sA = o;
-  if (mode != kModeTrue) o += r2_al16((size_t)T * nbd * 2);
+  if (apx && mode != kModeTrue) o += r2_al16((size_t)T * nbd * 2);
   L.sg = o;
-  if (mode == kModeExSign) o += r2_al16((size_t)T * nbd * 4);
+  if (apx && mode == kModeExSign) o += r2_al16((size_t)T * nbd * 4);
   L.vt = o;
-  o += r2_al16((size_t)D * vst);
+  if (part != 1) o += r2_al16((size_t)D * vst);
   L.vs = o;
-  o += r2_al16((size_t)ntb * D * 2);
+  if (part != 1) o += r2_al16((size_t)ntb * D * 2);
   L.waves = o;
   // top-k scratch (mxa_topk_lds.hpp layout), the P code row, P block exponents
   // and block maxima (16 each)
-  L.per_wave = r2_al16(topk_scratch_bytes(S)) + r2_al16((size_t)tpad) + 64 + 64;
+  L.per_wave = (part != 2 ? r2_al16(topk_scratch_bytes(S, k_top > 65)) : 0) +
+               (part != 1 ? r2_al16((size_t)tpad) + 64 + 64 : 0);
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
@@ -121,15 +128,19 @@ __device__ __forceinline__ double r2_dot(const int8_t* qrow, const int16_t* qs, 
   return acc;
 }
 
-template <int S, int MODE, bool TOPK, bool BIG>
-__global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
+template <int S, int MODE, bool TOPK, bool BIG, int PART>
+#ifndef MXA_SELECT_OCC
+#define MXA_SELECT_OCC 6  // selection kernel: waves per SIMD the register budget is sized for
+#endif
+__global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? MXA_SELECT_OCC : 1) void attn_rows2_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x;
   const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, vst = a.vst, ntb = a.ntb;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const Rows2Lds L = rows2_lds(MODE, T, D, kst, nbd, vst, ntb, S, a.tpad, TOPK ? a.k_top : 0, a.waves);
+  const Rows2Lds L = rows2_lds(MODE, T, D, kst, nbd, vst, ntb, S, a.tpad, TOPK ? a.k_top : 0, a.waves, PART);
+  constexpr bool kCodes = PART != 1 || MODE == kModeTrue, kApx = PART != 2, kFin = PART != 1;
   int8_t* tmx = reinterpret_cast<int8_t*>(smem + L.mx);
   int16_t* tsT = reinterpret_cast<int16_t*>(smem + L.sT);
   int8_t* top = reinterpret_cast<int8_t*>(smem + L.op);
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
   int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
   int16_t* tvs = reinterpret_cast<int16_t*>(smem + L.vs);
   unsigned char* wbase = smem + L.waves + (size_t)wave * L.per_wave;
-  const size_t tkb = topk_scratch_bytes(S);
+  const size_t tkb = PART == 2 ? 0 : topk_scratch_bytes(S, TOPK && BIG);
   int8_t* prow = reinterpret_cast<int8_t*>(wbase + r2_al16(tkb));
   int* pe = reinterpret_cast<int*>(wbase + r2_al16(tkb) + r2_al16(a.tpad));
   uint32_t* bm = reinterpret_cast<uint32_t*>(pe + 16);
@@ -148,35 +159,41 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
   const int64_t kb = (int64_t)bh * T;
   {
     const int cpr = a.dpad / 16;
-    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
-      const int j = i / cpr, c = i - j * cpr;
-      *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
-          *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
-      if (kOp)
-        *reinterpret_cast<uint4*>(top + (size_t)j * kst + 16 * c) =
-            *reinterpret_cast<const uint4*>(a.kop + (kb + j) * a.dpad + 16 * c);
+    if (kCodes || (kOp && kApx)) {
+      for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+        const int j = i / cpr, c = i - j * cpr;
+        if (kCodes)
+          *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
+              *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
+        if (kOp && kApx)
+          *reinterpret_cast<uint4*>(top + (size_t)j * kst + 16 * c) =
+              *reinterpret_cast<const uint4*>(a.kop + (kb + j) * a.dpad + 16 * c);
+      }
     }
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      tsT[i] = a.ksT[kb * nbd + i];
-      if (MODE != kModeTrue) tsA[i] = a.ksA[kb * nbd + i];
-      if (MODE == kModeExSign) tsg[i] = a.ksg[kb * nbd + i];
+      if (kCodes) tsT[i] = a.ksT[kb * nbd + i];
+      if (kApx && MODE != kModeTrue) tsA[i] = a.ksA[kb * nbd + i];
+      if (kApx && MODE == kModeExSign) tsg[i] = a.ksg[kb * nbd + i];
     }
-    const int vpr = a.tpad / 16;
-    const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
-    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
-      const int d = i / vpr, c = i - d * vpr;
-      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
-          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+    if (kFin) {
+      const int vpr = a.tpad / 16;
+      const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
+      for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
+        const int d = i / vpr, c = i - d * vpr;
+        *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
+            *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+      }
+      const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
+      for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];
+      for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(prow)[c] = 0u;
+      if (lane < 16) bm[lane] = 0u;
     }
-    const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
-    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];
-    for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(prow)[c] = 0u;
-    if (lane < 16) bm[lane] = 0u;
   }
   __syncthreads();
   MXA_PHASE(0);
 
-  for (int r = __builtin_amdgcn_readfirstlane(wave); r < a.N; r += a.waves) {
+  const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
+  for (int r = (int)blockIdx.y * a.rows_per_wg + __builtin_amdgcn_readfirstlane(wave); r < r_end; r += a.waves) {
     const int64_t grow = (int64_t)bh * a.N + r;
     const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
 
@@ -184,6 +201,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
 
     // ---- the row's T values in position order ------------------------------
     float vals[S];
+    if constexpr (PART != 2) {
     if (MXA_SKIP2(4)) {
 #pragma unroll
       for (int s = 0; s < S; ++s) vals[s] = (float)((64 * s + lane) & 7);
@@ -244,6 +262,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
         }
       }
     }
+    }  // PART != 2
 
     // the true score of key j for this row (bias included)
     auto true_of = [&](int j, bool& nan) -> float {
@@ -252,7 +271,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
       if (brow) t = t + brow[(int64_t)j * a.bs3];
       return t;
     };
-    if (MODE != kModeTrue && a.true_out) {  // debug output: every key's true score
+    if (kFin && MODE != kModeTrue && a.true_out) {  // debug output: every key's true score
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = 64 * s + lane;
@@ -267,6 +286,7 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
     MXA_PHASE(1);
     if constexpr (TOPK) {
       // ---- top-k in torch's CPU order ----------------------------------------
+      if constexpr (PART != 2) {
       RegTopk<S, BIG> tk;
       tk.init(wbase, T, lane);
 #pragma unroll
@@ -275,8 +295,50 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
         tk.I[s] = (uint32_t)(64 * s + lane);
       }
       if (!MXA_SKIP2(1)) {
+#ifdef MXA_PHASE_PROF
+        // run() split into its selection and sort halves for the phase counters
+        if (!tk.select(a.k_top)) {
+          MXA_PHASE(2);
+          const int m = a.k_top - 1;
+          if (m > 1) {
+            if (!BIG || m <= 64) tk.sort_head_win(m);
+            else {
+              tk.to_lds();
+              lds_sort_prefix_par<S>(tk.sc(), m, lane);
+            }
+          }
+        }
+        MXA_PHASE(6);
+#else
         tk.run(a.k_top);
+#endif
         tk.finalize();
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int pos = 64 * s + lane;
+        kept[s] = pos < a.k_top;
+        ix[s] = 0;
+        if (64 * s < a.k_top) {
+          ix[s] = kept[s] ? (int)tk.out_idx(s) : 0;
+          if (kept[s]) {
+            if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
+            if (PART == 1) a.idx32[grow * a.k_top + pos] = ix[s];
+          }
+        }
+      }
+      }  // PART != 2
+      if constexpr (PART == 1) {
+        MXA_PHASE(2);
+        continue;
+      }
+      if constexpr (PART == 2) {  // the kept indices of the selection kernel
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int pos = 64 * s + lane;
+          kept[s] = pos < a.k_top;
+          ix[s] = kept[s] ? a.idx32[grow * a.k_top + pos] : 0;
+        }
       }
       MXA_PHASE(2);
       // ---- vals = true.gather(idx); softmax ----------------------------------
@@ -284,14 +346,9 @@ __global__ __launch_bounds__(1024) void attn_rows2_kernel(Rows2Args a) {
       float mx = -INFINITY;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const int pos = 64 * s + lane;
-        kept[s] = pos < a.k_top;
-        ix[s] = 0;
         v[s] = -INFINITY;
         if (64 * s < a.k_top) {
-          ix[s] = kept[s] ? (int)tk.out_idx(s) : 0;
           if (kept[s]) {
-            if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
             bool nan = false;
             v[s] = MXA_SKIP2(8) ? (float)(ix[s] & 3) : true_of(ix[s], nan);
             mx = fmaxf(mx, v[s]);

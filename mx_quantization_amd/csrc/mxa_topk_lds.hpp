@@ -25,17 +25,19 @@ struct TopkLdsV2 {
   int* stk;       // [kTopkStack] introsort pending segments
 };
 
-// LDS bytes of one wave's scratch for rows of <= 64*S values (16-B multiple)
-__host__ __device__ constexpr size_t topk_scratch_bytes(int S) {
-  return (size_t)64 * S * 8 + (size_t)2 * 32 * S * 8 + (size_t)64 * S * 4 + (size_t)kTopkStack * 4 + 0;
+// LDS bytes of one wave's scratch for rows of <= 64*S values (16-B multiple).
+// big = false: no segment array (only the level-parallel sort of prefixes longer
+// than 64 uses it)
+__host__ __device__ constexpr size_t topk_scratch_bytes(int S, bool big = true) {
+  return (size_t)64 * S * 8 + (size_t)2 * 32 * S * 8 + (big ? (size_t)64 * S * 4 : 0) + (size_t)kTopkStack * 4 + 0;
 }
-__device__ __forceinline__ TopkLdsV2 carve_topk(unsigned char* base, int S) {
+__device__ __forceinline__ TopkLdsV2 carve_topk(unsigned char* base, int S, bool big = true) {
   TopkLdsV2 sc;
   sc.A = reinterpret_cast<uint64_t*>(base);
   sc.xa = sc.A + 64 * S;
   sc.xb = sc.xa + 32 * S;
   sc.seg = reinterpret_cast<uint32_t*>(sc.xb + 32 * S);
-  sc.stk = reinterpret_cast<int*>(sc.seg + 64 * S);
+  sc.stk = reinterpret_cast<int*>(sc.seg + (big ? 64 * S : 0));
   return sc;
 }
 

@@ -221,7 +221,7 @@ struct RegTopk {
   lds_i32* stk;  // [kTopkStack] pending introsort segments
 
   __device__ __forceinline__ void init(unsigned char* base, int n_, int lane_) {
-    const TopkLdsV2 t = carve_topk(base, S);
+    const TopkLdsV2 t = carve_topk(base, S, BIG);
     A = (lds_u64*)t.A;
     X = (lds_u64*)t.xa;
     seg = t.seg;

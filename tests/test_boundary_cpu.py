@@ -96,3 +96,31 @@ def test_product_refuses_cpu_tensors():
     q = torch.zeros(1, 1, 8, 64)
     with pytest.raises(NativeError):
         m.mx_topk_attention(q, q, q, 0.125, k_top=4)
+
+
+def _params(B, H, Nq, T, D, k, mode="ex_pred", top_k=1):
+    from mx_quantization_amd import _native as nat
+    p = nat.AttnParams()
+    p.q = p.k = p.v = p.out = 16  # non-null placeholders: the path query launches nothing
+    p.B, p.H, p.N, p.T, p.D, p.k_top = B, H, Nq, T, D, k
+    p.pred_mode, p.top_k, p.approx, p.scale = nat.PRED_MODES[mode], top_k, 1, 0.125
+    return p
+
+
+def test_attention_path_selection_is_host_logic():
+    """mxa_attention_path: split row kernels for top-k at every bench shape, the
+    fused row kernel for the dense softmax or on request (no launch, no GPU)."""
+    import ctypes
+    from mx_quantization_amd import _native as N
+    lib = N.lib()
+    split, fused = 3, 2
+    for shape in [(256, 12, 197, 197, 64, 20), (64, 16, 256, 256, 72, 154), (1, 3, 197, 197, 64, 20)]:
+        assert lib.mxa_attention_path(ctypes.byref(_params(*shape))) == split, shape
+    assert lib.mxa_attention_path(ctypes.byref(_params(8, 16, 256, 120, 72, 20, "MXINT4"))) == split
+    assert lib.mxa_attention_path(ctypes.byref(_params(1, 3, 197, 197, 64, 20, top_k=0))) == fused
+    os.environ["MXA_ATTN_PATH"] = "fused"
+    try:
+        assert lib.mxa_attention_path(ctypes.byref(_params(256, 12, 197, 197, 64, 20))) == fused
+    finally:
+        os.environ.pop("MXA_ATTN_PATH")
+    assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 600, 64, 5))) == -2  # T > 512

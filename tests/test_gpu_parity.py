@@ -259,15 +259,16 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
         assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
 
 
-PATHS = ("rows", "rows1", "tiles")
+PATHS = ("rows", "fused", "rows1", "tiles")
 
 
 def _attn_all_paths(M, q, k, v, scale, **kw):
-    """Run the fused op on every kernel path: the row kernel v2 with fused P.V
-    (default), the v1 row kernel + pv_kernel (MXA_ATTN_PATH=rows1) and the MFMA
-    score-tile kernel (MXA_ATTN_PATH=tiles)."""
+    """Run the op on every kernel path: the split row kernels v2 (selection kernel +
+    finishing kernel, the default for top-k), the one fused row kernel v2
+    (MXA_ATTN_PATH=fused), the v1 row kernel + pv_kernel (rows1) and the MFMA
+    score-tile kernel (tiles)."""
     res = []
-    for path in (None, "rows1", "tiles"):
+    for path in (None, "fused", "rows1", "tiles"):
         if path:
             os.environ["MXA_ATTN_PATH"] = path
         try:
