@@ -15,7 +15,7 @@ import os
 import torch  # noqa: F401  (must precede loading libmxa.so, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MXA_LIB", os.path.join(_HERE, "libmxa.so"))  # MXA_LIB: tools only
+LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(_HERE, "libmxa.so")  # MXA_LIB: tools only
 
 c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 

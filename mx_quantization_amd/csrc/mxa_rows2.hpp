@@ -216,18 +216,16 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? MXA_SELECT_OCC 
       }
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const int j = 64 * s + lane;
+        const int j = min(64 * s + lane, T - 1);  // clamped: no exec branch (positions >= T are never ranked)
         double acc = 0.0;
         bool nan = false;
-        if (j < T) {
 #pragma unroll
-          for (int b = 0; b < kMaxNB; ++b) {
-            if (b < nbd) {
-              const int e = exp_from16(tsA[j * nbd + b]);
-              if (e == kExpNaN || eq[b] == kExpNaN) nan = true;
-              const int m = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
-              acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
-            }
+        for (int b = 0; b < kMaxNB; ++b) {
+          if (b < nbd) {
+            const int e = exp_from16(tsA[j * nbd + b]);
+            nan = nan || e == kExpNaN || eq[b] == kExpNaN;
+            const int m = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
+            acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
           }
         }
         vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;

@@ -28,15 +28,18 @@ struct TopkLdsV2 {
 // LDS bytes of one wave's scratch for rows of <= 64*S values (16-B multiple).
 // big = false: no segment array (only the level-parallel sort of prefixes longer
 // than 64 uses it)
+// After xb: 64 per-lane trash entries, so that the exchange writes of lanes that
+// do not swap need no exec-mask branch (mxa_topk_reg.hpp exchange()).
 __host__ __device__ constexpr size_t topk_scratch_bytes(int S, bool big = true) {
-  return (size_t)64 * S * 8 + (size_t)2 * 32 * S * 8 + (big ? (size_t)64 * S * 4 : 0) + (size_t)kTopkStack * 4 + 0;
+  return (size_t)64 * S * 8 + (size_t)2 * 32 * S * 8 + (size_t)64 * 8 + (big ? (size_t)64 * S * 4 : 0) +
+         (size_t)kTopkStack * 4 + 0;
 }
 __device__ __forceinline__ TopkLdsV2 carve_topk(unsigned char* base, int S, bool big = true) {
   TopkLdsV2 sc;
   sc.A = reinterpret_cast<uint64_t*>(base);
   sc.xa = sc.A + 64 * S;
   sc.xb = sc.xa + 32 * S;
-  sc.seg = reinterpret_cast<uint32_t*>(sc.xb + 32 * S);
+  sc.seg = reinterpret_cast<uint32_t*>(sc.xb + 32 * S + 64);
   sc.stk = reinterpret_cast<int*>(sc.seg + (big ? 64 * S : 0));
   return sc;
 }

@@ -85,17 +85,16 @@ __device__ __forceinline__ void uset(V& a, int pos, uint32_t val) {
 // The swap exchange of one Hoare partition: the t-th swapping left stop and the
 // t-th swapping right stop (counted from the right) trade places.  Left stops
 // publish at X[t], right stops at X[half + t]; each reads its partner's slot.
-__device__ __forceinline__ void exchange(uint32_t& k, uint32_t& i, bool swl, bool swr, int rank, lds_u64* X, int half) {
-  if (swl || swr) {
-    const int wi = swl ? rank : half + rank;
-    X[wi] = pack_ki(k, i);
-  }
+// Branch-free: lanes that do not swap write and read their own trash entry
+// X[2 half + lane] (no exec-mask save / restore on the SALU).
+__device__ __forceinline__ void exchange(uint32_t& k, uint32_t& i, bool swl, bool swr, int rank, lds_u64* X, int half,
+                                         int lane) {
+  const bool sw = swl || swr;
+  X[sw ? (swl ? rank : half + rank) : 2 * half + lane] = pack_ki(k, i);
   wave_lds_sync();
-  if (swl || swr) {
-    const uint64_t v = X[swl ? half + rank : rank];
-    k = (uint32_t)(v >> 32);
-    i = (uint32_t)v;
-  }
+  const uint64_t v = X[sw ? (swl ? half + rank : rank) : 2 * half + lane];
+  k = (uint32_t)(v >> 32);
+  i = (uint32_t)v;
 }
 
 // ---- one partition step on the 64-wide window -------------------------------
@@ -126,7 +125,7 @@ __device__ __forceinline__ int win_step(RWin& w, int f, int l, lds_u64* X, int h
   const uint64_t SWL = ballot64(u > a) & Lb, SWR = ballot64(a > u) & Rb;
   if (SWL) {
     const bool swl = __builtin_amdgcn_inverse_ballot_w64(SWL);
-    exchange(w.k, w.i, swl, __builtin_amdgcn_inverse_ballot_w64(SWR), swl ? a : u, X, half);
+    exchange(w.k, w.i, swl, __builtin_amdgcn_inverse_ballot_w64(SWR), swl ? a : u, X, half, lane);
   }
   // cut = min(first non-swapping left stop, lowest swapping right stop | last)
   const uint64_t nsl = Lb & ~SWL;
@@ -177,19 +176,21 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
     rank[s] = __builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? a : u;
     anysw |= SWL[s];
   }
-  if (anysw) {
+  if (anysw) {  // branch-free per slot: non-swapping lanes write / read the trash entry
 #pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (__builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s]))
-        X[__builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? rank[s] : half + rank[s]] = pack_ki(K[s], I[s]);
+    for (int s = 0; s < S; ++s) {
+      const bool sw = __builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s]);
+      const bool swl = __builtin_amdgcn_inverse_ballot_w64(SWL[s]);
+      X[sw ? (swl ? rank[s] : half + rank[s]) : 2 * half + lane] = pack_ki(K[s], I[s]);
+    }
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (__builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s])) {
-        const uint64_t v = X[__builtin_amdgcn_inverse_ballot_w64(SWL[s]) ? half + rank[s] : rank[s]];
-        K[s] = (uint32_t)(v >> 32);
-        I[s] = (uint32_t)v;
-      }
+      const bool sw = __builtin_amdgcn_inverse_ballot_w64(SWL[s] | SWR[s]);
+      const bool swl = __builtin_amdgcn_inverse_ballot_w64(SWL[s]);
+      const uint64_t v = X[sw ? (swl ? half + rank[s] : rank[s]) : 2 * half + lane];
+      K[s] = sw ? (uint32_t)(v >> 32) : K[s];
+      I[s] = sw ? (uint32_t)v : I[s];
     }
   }
   int c1 = 1 << 20, c2 = l;
@@ -449,7 +450,7 @@ struct RegTopk {
         }
         --d;
         const int cut = win_step(w, f, l, X, half, lane);
-        if (lane == 0) stk[sp] = cut | (l << 10) | (d << 20);
+        stk[sp] = cut | (l << 10) | (d << 20);  // every lane the same value: no exec branch
         ++sp;
         l = cut;
       }
