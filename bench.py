@@ -243,7 +243,9 @@ def main():
         "config": {"workload": c["workload"], "batch_per_gpu": c["B"], "heads": c["H"], "seq": c["N"],
                    "keys": c["T"], "head_dim": c["D"], "k": c["k"], "pred_mode": c["mode"],
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "path": path, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": dom, "path": path,
+                     "limiter": ("instruction issue, scalar ALU (exact-order top-k partition steps; "
+                                 "PMC SQ_INSTS_SALU, profiles/r01_pmc_instr_*)") if dom in ("select", "fused") else None, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": by[dom], "mean_ms": stages[dom]},
         "stages_ms": stages,

@@ -123,17 +123,22 @@ __device__ __forceinline__ int exion_m(int raw) {
 }
 
 __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
-  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // 32-bit index math (the launcher checks rows * nb < 2^31): a 64-bit division
+  // is a ~50-instruction software sequence per thread, 32-bit ~10
+  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = threadIdx.x & 7;
-  const int64_t g = gt >> 3;
-  const int64_t ngroups = a.rows * a.nb;
+  const uint32_t g = gt >> 3;
+  const uint32_t ngroups = (uint32_t)(a.rows * a.nb);
   const bool valid = g < ngroups;
-  const int64_t row = valid ? g / a.nb : 0;
-  const int blk = valid ? (int)(g % a.nb) : 0;
-  const int64_t r = row % a.R;
-  const int64_t bh = row / a.R;
-  const int64_t h = bh % a.H;
-  const int64_t b = bh / a.H;
+  const uint32_t nb = (uint32_t)a.nb, R = (uint32_t)a.R, H = (uint32_t)a.H;
+  const uint32_t row32 = valid ? g / nb : 0u;
+  const int64_t row = row32;
+  const int blk = valid ? (int)(g - row32 * nb) : 0;
+  const uint32_t bh32 = row32 / R;
+  const int64_t r = row32 - bh32 * R;
+  const uint32_t b32 = bh32 / H;
+  const int64_t h = bh32 - b32 * H;
+  const int64_t b = b32;
   const float* xr = a.x + b * a.s0 + h * a.s1 + r * a.s2;
   const int c0 = blk * 32 + sub * 4;
   float xv[4];
@@ -228,15 +233,19 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
 // One thread per (matrix, block, column): coalesced along columns.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = a.mats * a.nb * a.C;
+  // 32-bit index math (the launcher checks the thread count fits)
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = (uint32_t)(a.mats * a.nb * a.C);
   if (t >= total) return;
-  const int c = (int)(t % a.C);
-  const int64_t mb_ = t / a.C;
-  const int blk = (int)(mb_ % a.nb);
-  const int64_t m = mb_ / a.nb;
-  const int64_t h = m % a.H;
-  const int64_t b = m / a.H;
+  const uint32_t C = (uint32_t)a.C, NB = (uint32_t)a.nb, H = (uint32_t)a.H;
+  const uint32_t mb_ = t / C;
+  const int c = (int)(t - mb_ * C);
+  const uint32_t m32 = mb_ / NB;
+  const int blk = (int)(mb_ - m32 * NB);
+  const uint32_t b32 = m32 / H;
+  const int64_t m = m32;
+  const int64_t h = m32 - b32 * H;
+  const int64_t b = b32;
   const float* xc = a.x + b * a.s0 + h * a.s1 + c;
   const int r0 = blk * 32;
   float xv[32];
@@ -413,12 +422,14 @@ namespace mxa {
 int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream) {
   const int64_t threads = a.rows * a.nb * 8;
   if (threads == 0) return MXA_OK;
+  if (a.rows * a.nb >= ((int64_t)1 << 28)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices (x8 lanes)
   hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream) {
   const int64_t threads = a.mats * a.nb * a.C;
   if (threads == 0) return MXA_OK;
+  if (threads >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices
   hipLaunchKernelGGL(cols_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
