@@ -135,14 +135,26 @@ __device__ __forceinline__ int win_step(RWin& w, int f, int l, lds_u64* X, int h
 }
 
 // ---- one partition step on the slot registers (ranges longer than 64) --------
+// A mirrors the row in LDS while the steps run on the slot registers (the caller
+// writes it before the first step; every step rewrites it): the pivot candidates
+// are broadcast LDS reads instead of S readlanes + selects each.
 template <int S>
 __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename SlotVec<S>::T& I, int f, int l,
-                                          lds_u64* X, int half, int lane) {
+                                          lds_u64* X, int half, int lane, lds_u64* A) {
   const int a_ = f + 1, b_ = f + (l - f) / 2, c_ = l - 1;
+  const uint64_t xa = A[a_], xb = A[b_], xc = A[c_], xf = A[f];
+  const uint32_t ka = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xa >> 32));
+  const uint32_t kb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xb >> 32));
+  const uint32_t kc = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xc >> 32));
   uint32_t p;
-  const int m = median3(uget(K, a_), uget(K, b_), uget(K, c_), a_, b_, c_, &p);
-  {
-    const uint32_t kf = uget(K, f), jf = uget(I, f), jm = uget(I, m);
+  const int m = median3(ka, kb, kc, a_, b_, c_, &p);
+  {  // iter_swap(first, median)
+    const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xf >> 32));
+    const uint32_t jf = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xf);
+    const uint32_t ja = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xa);
+    const uint32_t jb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xb);
+    const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xc);
+    const uint32_t jm = m == a_ ? ja : (m == b_ ? jb : jc);
     uset(K, f, p);
     uset(I, f, jm);
     uset(K, m, kf);
@@ -193,6 +205,10 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
       I[s] = sw ? (uint32_t)v : I[s];
     }
   }
+  // the mirror for the next step
+#pragma unroll
+  for (int s = 0; s < S; ++s) A[64 * s + lane] = pack_ki(K[s], I[s]);
+  wave_lds_sync();
   int c1 = 1 << 20, c2 = l;
 #pragma unroll
   for (int s = S - 1; s >= 0; --s) {
@@ -325,6 +341,7 @@ struct RegTopk {
       return true;
     }
     int first = 0, last = n;
+    bool mirror = false;  // A holds the row (slots_step's pivot reads)
     const int nth = k - 1;
     int depth = 2 * ilog2(n);
     while (last - first > 3) {
@@ -345,7 +362,12 @@ struct RegTopk {
         if (mode != kWin) to_win(win_base(first));
         cut = win_step(w, first, last, X, half, lane);
       } else {
-        cut = slots_step<S>(K, I, first, last, X, half, lane);
+        if (!mirror) {
+          slots_to_lds();
+          wave_lds_sync();
+          mirror = true;
+        }
+        cut = slots_step<S>(K, I, first, last, X, half, lane, A);
       }
       if (cut <= nth) first = cut;
       else last = cut;
@@ -379,6 +401,7 @@ struct RegTopk {
       return t;
     }
     int first = 0, last = n;
+    bool mirror = false;  // A holds the row (slots_step's pivot reads)
     const int nth = k - 1;
     int depth = 2 * ilog2(n);
     while (last - first > 3 && last > W) {
@@ -399,7 +422,12 @@ struct RegTopk {
         if (mode != kWin) to_win(win_base(first));
         cut = win_step(w, first, last, X, half, lane);
       } else {
-        cut = slots_step<S>(K, I, first, last, X, half, lane);
+        if (!mirror) {
+          slots_to_lds();
+          wave_lds_sync();
+          mirror = true;
+        }
+        cut = slots_step<S>(K, I, first, last, X, half, lane, A);
       }
       if (cut <= nth) first = cut;
       else last = cut;
@@ -463,19 +491,24 @@ struct RegTopk {
       d = e >> 20;
     }
     // stable rank of every position of [0, m): keys greater, or equal and earlier
+    // (4 positions per loop trip: the loop control is scalar work; lanes >= m
+    // write / read their trash entry, no exec branch)
     const uint32_t mk = w.k;
     int r = 0;
-    for (int j = 0; j < m; ++j) {
-      const uint32_t kj = rdl(w.k, j);
-      r += (kj > mk || (kj == mk && j < lane)) ? 1 : 0;
+    for (int j0 = 0; j0 < m; j0 += 4) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = j0 + t;
+        const uint32_t kj = rdl(w.k, j & 63);
+        r += (j < m && (kj > mk || (kj == mk && j < lane))) ? 1 : 0;
+      }
     }
-    if (lane < m) X[r] = pack_ki(w.k, w.i);
+    const bool in = lane < m;
+    X[in ? r : 2 * half + lane] = pack_ki(w.k, w.i);
     wave_lds_sync();
-    if (lane < m) {
-      const uint64_t v = X[lane];
-      w.k = (uint32_t)(v >> 32);
-      w.i = (uint32_t)v;
-    }
+    const uint64_t v = X[in ? lane : 2 * half + lane];
+    w.k = (uint32_t)(v >> 32);
+    w.i = (uint32_t)v;
     wave_lds_sync();
   }
 
