@@ -575,6 +575,7 @@ __global__ __launch_bounds__(64 * kRowsWaves, 4) void attn_rows_kernel(RowsArgs 
 
 }  // namespace mxa
 #include "mxa_rows2.hpp"
+#include "mxa_finish.hpp"
 namespace mxa {
 
 struct PVArgs {
@@ -1000,6 +1001,32 @@ static int launch_rows2_p(const Rows2Args& ra0, int BH, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
+// finishing kernel with P.V on int8 MFMA (mxa_finish.hpp): 16-row tiles, <= 8 key blocks
+// Opt-in (MXA_FINISH=mfma): measured slower than the per-row v_dot4 finishing kernel
+// at the bench shapes (DeiT-base 0.70 vs 0.55 ms: its 16-row P tiles in LDS cut the
+// occupancy to 12 waves per CU, and the per-row gather / softmax dominate anyway).
+static bool finish_mfma_ok(const Rows2Args& ra) {
+  const char* env = getenv("MXA_FINISH");
+  if (!env || std::string(env) != "mfma") return false;
+  return ra.ntb <= 8 && fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.tpad).total <= 160 * 1024;
+}
+template <int S>
+static int launch_finish(const Rows2Args& ra0, int BH, hipStream_t stream) {
+  Rows2Args ra = ra0;
+  ra.waves = kFinWaves;
+  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.tpad).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_finish_kernel<S>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  // rows per workgroup: whole 16-row tiles; few heads -> split the rows over grid.y
+  const int tiles = (ra.N + 15) / 16;
+  const int chunks = std::max(1, std::min((tiles + kFinWaves - 1) / kFinWaves, 1024 / std::max(BH, 1)));
+  ra.rows_per_wg = 16 * ((tiles + chunks - 1) / chunks);
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL((attn_finish_kernel<S>), dim3((unsigned)BH, gy), dim3(64 * kFinWaves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
 // split: the selection kernel, an event, the finishing kernel
 template <int S, int MODE, bool TOPK, bool BIG>
 static int launch_rows2_b(const Rows2Args& ra, int BH, bool split, hipStream_t stream, hipEvent_t* ev) {
@@ -1008,7 +1035,7 @@ static int launch_rows2_b(const Rows2Args& ra, int BH, bool split, hipStream_t s
     rc = launch_rows2_p<S, MODE, TOPK, BIG, 1>(ra, BH, stream);
     if (rc) return rc;
     if (ev) (void)hipEventRecord(ev[4], stream);
-    rc = launch_rows2_p<S, MODE, TOPK, BIG, 2>(ra, BH, stream);
+    rc = finish_mfma_ok(ra) ? launch_finish<S>(ra, BH, stream) : launch_rows2_p<S, MODE, TOPK, BIG, 2>(ra, BH, stream);
   } else {
     rc = launch_rows2_p<S, MODE, TOPK, BIG, 0>(ra, BH, stream);
     if (ev) (void)hipEventRecord(ev[4], stream);

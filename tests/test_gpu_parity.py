@@ -345,6 +345,26 @@ def test_approx_modes_all_paths_vs_oracle(M, mode, N, T, k):
         _check_vs_oracle(got, r, name)
 
 
+@pytest.mark.parametrize("D,N,T,k,mode", [(64, 197, 197, 20, "ex_pred"), (72, 256, 256, 154, "ex_pred"),
+                                          (72, 77, 120, 20, "MXINT4"), (72, 33, 120, 77, "two_step_leading_ones")])
+def test_finish_mfma_kernel_vs_oracle(M, D, N, T, k, mode):
+    """The int8-MFMA finishing kernel (MXA_FINISH=mfma: P.V over 16-row tiles, one
+    v_mfma_i32_16x16x32_i8 per 32-key MX block, fp64 block epilogue), partial tiles."""
+    rng = np.random.default_rng(13)
+    B, H = 1, 3
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    os.environ["MXA_FINISH"] = "mfma"
+    try:
+        got = M.mx_topk_attention(dev(q), dev(kk), dev(v), D ** -0.5, k_top=k, pred_mode=mode, return_scores=True)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("MXA_FINISH", None)
+    r = O.attention(q, kk, v, D ** -0.5, k_top=k, pred_mode=mode)
+    _check_vs_oracle([host(t) for t in got], r, "finish_mfma")
+
+
 def test_pixart_cross_full_batch(M):
     B, H, N, T, D, k = 8, 16, 256, 120, 72, 20
     rng = np.random.default_rng(0)
