@@ -104,22 +104,34 @@ struct RWin {
   uint32_t i;  // index of position b + lane
 };
 
+// a uniform scalar copied into a VGPR the compiler treats as divergent: the logic
+// on it is issued on the VALU (the scalar unit is the selection kernel's limiter)
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
+  uint32_t v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+  return v;
+}
+
 __device__ __forceinline__ int win_step(RWin& w, int f, int l, lds_u64* X, int half, int lane) {
   const int rf = f - w.b, rl = l - w.b;
   const int ra = rf + 1, rb = rf + (l - f) / 2, rc = rl - 1;
-  uint32_t p;
-  const int rm = median3(rdl(w.k, ra), rdl(w.k, rb), rdl(w.k, rc), ra, rb, rc, &p);
+  // __move_median_to_first on the VALU: branch-free selects on VGPR copies
+  const uint32_t ka = to_vgpr(rdl(w.k, ra)), kb = to_vgpr(rdl(w.k, rb)), kc = to_vgpr(rdl(w.k, rc));
+  const bool ab = ka > kb, bc = kb > kc, ac = ka > kc;
+  const int rmv = ab ? (bc ? rb : (ac ? rc : ra)) : (ac ? ra : (bc ? rc : rb));
+  const uint32_t p = ab ? (bc ? kb : (ac ? kc : ka)) : (ac ? ka : (bc ? kc : kb));
+  const int rm = __builtin_amdgcn_readfirstlane(rmv);
   {  // iter_swap(first, median)
     const uint32_t kf = rdl(w.k, rf), jf = rdl(w.i, rf), jm = rdl(w.i, rm);
-    w.k = wrl(w.k, p, rf);
-    w.i = wrl(w.i, jm, rf);
-    w.k = wrl(w.k, kf, rm);
-    w.i = wrl(w.i, jf, rm);
+    const bool atf = lane == rf, atm = lane == rm;
+    w.k = atf ? p : (atm ? kf : w.k);
+    w.i = atf ? jm : (atm ? jf : w.i);
   }
-  // stops as lane masks: compares straight to SGPRs, the range by SALU
-  const uint64_t rng = range_mask64(rf, rl);
-  const uint64_t Lb = ballot64(!(w.k > p)) & rng & ~(1ull << rf);  // left stops in [first+1, last)
-  const uint64_t Rb = ballot64(!(p > w.k)) & rng;                   // right stops in [first, last)
+  // stops as lane masks straight from VALU compares (ranges as lane offsets)
+  const uint64_t inl = ballot64((unsigned)(lane - rf - 1) < (unsigned)(rl - rf - 1));  // [first+1, last)
+  const uint64_t inr = ballot64((unsigned)(lane - rf) < (unsigned)(rl - rf));          // [first, last)
+  const uint64_t Lb = ballot64(!(w.k > p)) & inl;  // left stops
+  const uint64_t Rb = ballot64(!(p > w.k)) & inr;  // right stops
   const int a = mbcnt(Lb);                                          // left stops below
   const int u = (int)__popcll(Rb) - mbcnt_incl(Rb);                 // right stops above
   const uint64_t SWL = ballot64(u > a) & Lb, SWR = ballot64(a > u) & Rb;
@@ -143,11 +155,13 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
                                           lds_u64* X, int half, int lane, lds_u64* A) {
   const int a_ = f + 1, b_ = f + (l - f) / 2, c_ = l - 1;
   const uint64_t xa = A[a_], xb = A[b_], xc = A[c_], xf = A[f];
-  const uint32_t ka = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xa >> 32));
-  const uint32_t kb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xb >> 32));
-  const uint32_t kc = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xc >> 32));
-  uint32_t p;
-  const int m = median3(ka, kb, kc, a_, b_, c_, &p);
+  // __move_median_to_first on the VALU (branch-free selects on the broadcast values)
+  uint32_t ka = (uint32_t)(xa >> 32), kb = (uint32_t)(xb >> 32), kc = (uint32_t)(xc >> 32);
+  asm volatile("" : "+v"(ka), "+v"(kb), "+v"(kc));
+  const bool ab = ka > kb, bc = kb > kc, ac = ka > kc;
+  const int mv = ab ? (bc ? b_ : (ac ? c_ : a_)) : (ac ? a_ : (bc ? c_ : b_));
+  const uint32_t p = ab ? (bc ? kb : (ac ? kc : ka)) : (ac ? ka : (bc ? kc : kb));
+  const int m = __builtin_amdgcn_readfirstlane(mv);
   {  // iter_swap(first, median)
     const uint32_t kf = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xf >> 32));
     const uint32_t jf = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xf);
@@ -167,9 +181,10 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int pos = 64 * s + lane;
-    const uint64_t inr = ballot64(pos >= f) & ballot64(pos < l);
-    Lb[s] = inr & ballot64(!(K[s] > p)) & ~ballot64(pos == f);  // left stops in [first+1, last)
-    Rb[s] = inr & ballot64(!(p > K[s]));                         // right stops in [first, last)
+    const uint64_t inl = ballot64((unsigned)(pos - f - 1) < (unsigned)(l - f - 1));  // [first+1, last)
+    const uint64_t inr = ballot64((unsigned)(pos - f) < (unsigned)(l - f));          // [first, last)
+    Lb[s] = inl & ballot64(!(K[s] > p));  // left stops
+    Rb[s] = inr & ballot64(!(p > K[s]));  // right stops
     cl[s] = totL;
     cr[s] = totR;
     totL += (int)__popcll(Lb[s]);
