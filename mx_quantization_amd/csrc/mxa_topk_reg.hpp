@@ -224,14 +224,17 @@ __device__ __forceinline__ int slots_step(typename SlotVec<S>::T& K, typename Sl
 #pragma unroll
   for (int s = 0; s < S; ++s) A[64 * s + lane] = pack_ki(K[s], I[s]);
   wave_lds_sync();
-  int c1 = 1 << 20, c2 = l;
+  // cut = min(first non-swapping left stop, lowest swapping right stop | last):
+  // per-lane candidates and a DPP min-reduction (VALU) instead of per-slot s_ff1
+  uint32_t cand = 1u << 20;
 #pragma unroll
-  for (int s = S - 1; s >= 0; --s) {
-    const uint64_t nsl = Lb[s] & ~SWL[s];
-    if (nsl) c1 = 64 * s + ffs64(nsl);
-    if (SWR[s]) c2 = 64 * s + ffs64(SWR[s]);
+  for (int s = 0; s < S; ++s) {
+    const uint32_t pos = (uint32_t)(64 * s + lane);
+    cand = min(cand, __builtin_amdgcn_inverse_ballot_w64(Lb[s] & ~SWL[s]) ? pos : (1u << 20));
+    cand = min(cand, __builtin_amdgcn_inverse_ballot_w64(SWR[s]) ? pos : (1u << 20));
   }
-  return c1 < c2 ? c1 : c2;
+  const int c = (int)wave_reduce(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+  return c < l ? c : l;
 }
 
 // ---- row state ---------------------------------------------------------------
