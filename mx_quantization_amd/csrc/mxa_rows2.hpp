@@ -132,7 +132,7 @@ template <int S, int MODE, bool TOPK, bool BIG, int PART>
 #ifndef MXA_SELECT_OCC
 #define MXA_SELECT_OCC 6  // selection kernel: waves per SIMD the register budget is sized for
 #endif
-__global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? MXA_SELECT_OCC : 1) void attn_rows2_kernel(Rows2Args a) {
+__global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELECT_OCC - 1 : MXA_SELECT_OCC) : 1) void attn_rows2_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
