@@ -67,3 +67,28 @@ def test_bench_single_rank_timed_region_has_no_collectives():
     e = bench.timed_region(lambda: calls.append(1), 1, lambda: calls.append(0), torch.device("cpu"))
     assert calls == [0, 1, 0] and e >= 0.0
     assert not dist.is_initialized()
+
+
+def test_bench_stage_bytes_by_path():
+    """Algorithmic bytes per kernel: the split path's two kernels move
+    the fused kernel's inputs plus the 4-byte kept indices written once and read once."""
+    import bench
+    c = bench.CONFIGS["deit_base"]
+    split = bench.stage_bytes(c, "rows_split")
+    fused = bench.stage_bytes(c, "rows_fused")
+    h, N, k = c["B"] * c["H"], c["N"], c["k"]
+    assert list(split)[:3] == list(fused)[:3] == ["rows_prep_q", "rows_prep_k", "cols_prep_v"]
+    assert split["select"] + split["finish"] == fused["fused"] + h * 8 * N * k
+    assert bench.fused_min_bytes(c) == 716537856  # SURVEY.md §8d: 716.5 MB at DeiT-base b256
+
+
+def test_hbm_traffic_kernel_names_map_to_bench_stages():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("hbm_traffic", os.path.join(ROOT, "tools", "hbm_traffic.py"))
+    ht = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ht)
+    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, false, 1>(mxa::Rows2Args)") == "select"
+    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, true, 2>(mxa::Rows2Args)") == "finish"
+    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 0, false, false, 0>(mxa::Rows2Args)") == "fused"
+    assert ht.stage_of("mxa::rows_prep_kernel(mxa::RowsPrepArgs)") == "rows_prep"
+    assert ht.stage_of("mxa::cols_prep_kernel(mxa::ColsPrepArgs)") == "cols_prep_v"
