@@ -975,6 +975,17 @@ static int rows2_waves(int mode, bool topk, const Rows2Args& ra, int S, int part
     return w <= wmax && rows2_total(mode, topk, ra, S, w, part) <= 160 * 1024 ? w : 0;
   }
   if (part == 1) return rows2_total(mode, topk, ra, S, 4, part) <= 160 * 1024 ? 4 : 0;
+  if (part == 2) {
+    // finishing kernel: the workgroup size that keeps the most waves resident per CU
+    // (LDS-limited workgroups x waves, capped by its 7-waves-per-SIMD register use):
+    // DeiT-base 8 (tie), DiT 16 (larger K / V tables: 2 workgroups per CU either way)
+    auto resident = [&](int w) {
+      const size_t t = rows2_total(mode, topk, ra, S, w, part);
+      return t > 160 * 1024 ? 0 : std::min((int)(160 * 1024 / t) * w, 28);
+    };
+    const int r8 = resident(8), r16 = resident(16);
+    if (r8 > 0 || r16 > 0) return r16 > r8 ? 16 : 8;
+  }
   if (rows2_total(mode, topk, ra, S, 8, part) <= 80 * 1024) return 8;
   if (rows2_total(mode, topk, ra, S, 16, part) <= 160 * 1024) return 16;
   if (rows2_total(mode, topk, ra, S, 8, part) <= 160 * 1024) return 8;
