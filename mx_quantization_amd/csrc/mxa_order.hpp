@@ -1,26 +1,30 @@
-// Lane-per-row tail of the exact-order top-k.
+// Order keys and the serial libstdc++ 11 helpers of the exact-order top-k.
 //
-// The wave-wide restatement (mxa_topk_reg.hpp) spends ~100 wave instructions on
-// every partition step whatever the range length, and most steps of torch's CPU
-// topk run on short ranges (DeiT-base, k = 20: ~5 of ~7 introselect steps are on
-// <= 64 positions, and std::sort of the k-1 prefix is all short ranges).  Those
-// steps are cheaper as plain serial code, one ROW per LANE: the wave-wide pass
-// narrows each row until its pending work lies inside positions [0, W), parks that
-// window in LDS, and afterwards every lane runs libstdc++ 11 itself on its own
-// window -- the same element movements as torch's build, one
-// instruction stream amortised over up to 64 rows.
-//
-// Followed literally (stl_algo.h / stl_heap.h of GCC 11, the code behind
-// aten/src/ATen/native/TopKImpl.h:45-86):
-//   __introselect, __unguarded_partition_pivot, __move_median_to_first,
-//   __unguarded_partition, __insertion_sort (== __final_insertion_sort's two
-//   halves: the unguarded half stops at the same element), __introsort_loop,
-//   __partial_sort (heap fallback), __heap_select, __sort_heap.
-// Elements are pack_ki(order key, index); comp(x, y) = key(x) > key(y).
+// torch.topk on CPU (aten/src/ATen/native/TopKImpl.h:45-86) sorts pair<double,int64>
+// with cmp(x, y) = (isnan(x) && !isnan(y)) || x > y.  Here an element is
+// pack_ki(order key, index) and cmp is an unsigned compare of the keys.
+// The serial helpers below follow stl_heap.h / stl_algo.h of GCC 11 literally (the
+// code behind torch's build); the group top-k (mxa_topk_grp.hpp) runs
+// them on one lane of a row for the rare paths: depth-limit heap fallbacks,
+// partial_sort (k*64 <= n) and __insertion_sort of <= 3 elements.
 #pragma once
-#include "mxa_topk.hpp"
+#include "mxa_common.hpp"
 
 namespace mxa {
+
+// Order-preserving key for cmp: NaN largest (all NaNs tie), -0 == +0.  Every key
+// of a real element is >= 0x007FFFFF (-inf), so 0 sorts after all of them.
+__device__ __forceinline__ uint32_t order_key(float f) {
+  uint32_t b = __float_as_uint(f);
+  const uint32_t a = b & 0x7FFFFFFFu;
+  if (a > 0x7F800000u) return 0xFFFFFFFFu;
+  if (a == 0u) b = 0u;
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__device__ __forceinline__ uint64_t pack_ki(uint32_t key, uint32_t idx) { return ((uint64_t)key << 32) | idx; }
+
+__device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
 
 typedef __attribute__((address_space(3))) uint64_t lu64;
 typedef __attribute__((address_space(3))) int li32;
@@ -126,62 +130,6 @@ __device__ __forceinline__ int ln_partition_pivot(lu64* a, int f, int l) {
     a[i] = xj;
     a[j] = xi;
     ++i;
-  }
-}
-
-// state of a row handed from the wave-wide pass to its lane
-struct LaneTask {
-  int first, last, depth;  // pending __introselect range (first == last: done)
-  int nth, k;              // k - 1 == nth; the sorted prefix is [0, k - 1)
-};
-
-// __introselect's remainder on [first, last), then std::sort of [0, m), m = k - 1
-// (TopKImpl.h:45-86): __introsort_loop down to 16-element segments with the depth
-// limit, each segment finished by the (stable) insertion sort.  stk: this lane's
-// stack of pending segments (>= 2 * lg(m) entries).
-__device__ inline void lane_topk_tail(lu64* a, LaneTask t, li32* stk) {
-  int first = t.first, last = t.last, depth = t.depth;
-  const int nth = t.nth;
-  bool sel_done = first == last;
-  while (!sel_done && last - first > 3) {
-    if (depth == 0) {  // __heap_select(first, nth + 1, last); iter_swap(first, nth)
-      ln_heap_select(a, first, nth + 1, last);
-      const uint64_t x = a[first];
-      a[first] = a[nth];
-      a[nth] = x;
-      sel_done = true;
-      break;
-    }
-    --depth;
-    const int cut = ln_partition_pivot(a, first, last);
-    if (cut <= nth) first = cut;
-    else last = cut;
-  }
-  if (!sel_done) ln_insertion_sort(a, first, last);
-
-  const int m = t.k - 1;  // std::sort(begin, begin + k - 1)
-  if (m < 2) return;
-  int sp = 0;
-  int f = 0, l = m, d = 2 * ilog2(m);
-  while (true) {
-    while (l - f > 16) {
-      if (d == 0) {  // std::__partial_sort(f, l, l): heapsort of the segment
-        ln_heap_select(a, f, l, l);
-        ln_sort_heap(a, f, l);
-        f = l;
-        break;
-      }
-      --d;
-      const int cut = ln_partition_pivot(a, f, l);
-      stk[sp++] = cut | (l << 10) | (d << 20);  // __introsort_loop(cut, last, depth)
-      l = cut;
-    }
-    if (l - f > 1) ln_insertion_sort(a, f, l);
-    if (sp == 0) break;
-    const int e = stk[--sp];
-    f = e & 1023;
-    l = (e >> 10) & 1023;
-    d = e >> 20;
   }
 }
 

@@ -1,24 +1,19 @@
-// Row-oriented fused attention kernel, version 2: scores -> exact-order top-k ->
-// softmax -> P quantization -> P.V, one wave per query row, nothing of the row
-// leaves the CU but the output and the kept indices.
-//
-// Per workgroup (one head): the head's K tables (MXINT8 codes + exponents, the
-// approximator operands) and V^T codes + exponents are staged in LDS once.  Per
-// query row (one wave):
-//   1. the T approximate (or true) scores land in registers in position order
-//      (lane i, slot s <-> key 64 s + i) -- exact fp64 block epilogue;
-//   2. RegTopk (mxa_topk_reg.hpp) reproduces torch's CPU topk index order;
-//   3. lane l < k recomputes the true score of the l-th kept key (v_dot4 over the
-//      LDS codes), softmax over the kept scores (DPP reductions);
-//   4. P is MX-quantized along keys (block maxima by LDS atomic max) into a dense
-//      LDS code row that holds zeros everywhere else;
-//   5. out[d] = sum_b 2^(eP_b + eV_bd) * sum_{t in b} P_t V_td: v_dot4 of the P row
-//      (broadcast reads) against lane d's V^T row, exact fp64 block epilogue.
+// Row kernels of the attention core, one wave per query row:
+//   PART 2, the finishing kernel of the top-k path: for the k kept indices of the row
+//      (select_kernel, mxa_select.hpp) lane l < k recomputes the true score of the l-th
+//      kept key (v_dot4 over the LDS codes, exact fp64 block epilogue),
+//      softmax over the kept scores (DPP reductions), P MX-quantized along keys (block
+//      maxima by LDS atomic max) into a dense LDS code row that is zero elsewhere, and
+//      out[d] = sum_b 2^(eP_b + eV_bd) * sum_{t in b} P_t V_td (v_dot4 of the P row
+//      against lane d's V^T row, fp64 block epilogue);
+//   PART 0, the dense branch (top_k=False): all T true scores, softmax, MX(P), P.V.
+// The head's K codes + exponents and V^T codes + exponents are staged in LDS once
+// per workgroup.
 // Callers: workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
 // workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859; the MX matmul
 // of P.V: microxscaling/mx/matmul.py:68-76.
 #pragma once
-#include "mxa_topk_reg.hpp"
+#include "mxa_order.hpp"
 
 namespace mxa {
 
@@ -48,14 +43,8 @@ struct Rows2Args {
   int waves;        // waves per workgroup
   int rows_per_wg;  // query rows per workgroup (grid.y splits a head when there are few heads)
   int32_t* idx32;  // split path: the kept indices [B*H*N][k_top] between the two kernels
-  int dbg;    // instrumented build only: phases to skip (tools/skip_prof.py), 0 otherwise
 };
 
-#ifdef MXA_PHASE_PROF
-#define MXA_SKIP2(bit) (a.dbg & (bit))
-#else
-#define MXA_SKIP2(bit) false
-#endif
 
 struct Rows2Lds {
   size_t mx, sT, op, sA, sg, vt, vs, waves, per_wave, total;
@@ -88,8 +77,7 @@ __host__ __device__ inline Rows2Lds rows2_lds(int mode, int T, int D, int kst, i
   L.waves = o;
   // top-k scratch (mxa_topk_lds.hpp layout), the P code row, P block exponents
   // and block maxima (16 each)
-  L.per_wave = (part != 2 ? r2_al16(topk_scratch_bytes(S, k_top > 65)) : 0) +
-               (part != 1 ? r2_al16((size_t)tpad) + 64 + 64 : 0);
+  L.per_wave = part != 1 ? r2_al16((size_t)tpad) + 64 + 64 : 0;
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
@@ -128,11 +116,11 @@ __device__ __forceinline__ double r2_dot(const int8_t* qrow, const int16_t* qs, 
   return acc;
 }
 
+// PART 0: the dense branch (top_k=False: softmax over every key); PART 2: the
+// finishing kernel of the top-k path (the kept indices come from select_kernel)
 template <int S, int MODE, bool TOPK, bool BIG, int PART>
-#ifndef MXA_SELECT_OCC
-#define MXA_SELECT_OCC 6  // selection kernel: waves per SIMD the register budget is sized for
-#endif
-__global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELECT_OCC - 1 : MXA_SELECT_OCC) : 1) void attn_rows2_kernel(Rows2Args a) {
+__global__ __launch_bounds__(1024, 1) void attn_rows2_kernel(Rows2Args a) {
+  static_assert(PART == 0 || PART == 2, "part 1 is select_kernel (mxa_select.hpp)");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -149,13 +137,11 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
   int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
   int16_t* tvs = reinterpret_cast<int16_t*>(smem + L.vs);
   unsigned char* wbase = smem + L.waves + (size_t)wave * L.per_wave;
-  const size_t tkb = PART == 2 ? 0 : topk_scratch_bytes(S, TOPK && BIG);
-  int8_t* prow = reinterpret_cast<int8_t*>(wbase + r2_al16(tkb));
-  int* pe = reinterpret_cast<int*>(wbase + r2_al16(tkb) + r2_al16(a.tpad));
+  int8_t* prow = reinterpret_cast<int8_t*>(wbase);
+  int* pe = reinterpret_cast<int*>(wbase + r2_al16(a.tpad));
   uint32_t* bm = reinterpret_cast<uint32_t*>(pe + 16);
 
   // ---- stage the head's K and V tables ---------------------------------------
-  MXA_PHASE_INIT();
   const int64_t kb = (int64_t)bh * T;
   {
     const int cpr = a.dpad / 16;
@@ -190,7 +176,6 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
     }
   }
   __syncthreads();
-  MXA_PHASE(0);
 
   const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
   for (int r = (int)blockIdx.y * a.rows_per_wg + __builtin_amdgcn_readfirstlane(wave); r < r_end; r += a.waves) {
@@ -202,10 +187,7 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
     // ---- the row's T values in position order ------------------------------
     float vals[S];
     if constexpr (PART != 2) {
-    if (MXA_SKIP2(4)) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) vals[s] = (float)((64 * s + lane) & 7);
-    } else if constexpr (MODE == kModeExSign) {
+    if constexpr (MODE == kModeExSign) {
       // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
       uint32_t sq[kMaxNB];
       int eq[kMaxNB];
@@ -281,64 +263,14 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
 
     int ix[S];
     bool kept[S];
-    MXA_PHASE(1);
     if constexpr (TOPK) {
-      // ---- top-k in torch's CPU order ----------------------------------------
-      if constexpr (PART != 2) {
-      RegTopk<S, BIG> tk;
-      tk.init(wbase, T, lane);
+      static_assert(PART == 2, "top-k rows are selected by select_kernel (mxa_select.hpp)");
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        tk.K[s] = order_key(vals[s]);
-        tk.I[s] = (uint32_t)(64 * s + lane);
-      }
-      if (!MXA_SKIP2(1)) {
-#ifdef MXA_PHASE_PROF
-        // run() split into its selection and sort halves for the phase counters
-        if (!tk.select(a.k_top)) {
-          MXA_PHASE(2);
-          const int m = a.k_top - 1;
-          if (m > 1) {
-            if (!BIG || m <= 64) tk.sort_head_win(m);
-            else {
-              tk.to_lds();
-              lds_sort_prefix_par<S>(tk.sc(), m, lane);
-            }
-          }
-        }
-        MXA_PHASE(6);
-#else
-        tk.run(a.k_top);
-#endif
-        tk.finalize();
-      }
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
+      for (int s = 0; s < S; ++s) {  // the kept indices of the selection kernel
         const int pos = 64 * s + lane;
         kept[s] = pos < a.k_top;
-        ix[s] = 0;
-        if (64 * s < a.k_top) {
-          ix[s] = kept[s] ? (int)tk.out_idx(s) : 0;
-          if (kept[s]) {
-            if (a.idx_out) a.idx_out[grow * a.k_top + pos] = (int64_t)ix[s];
-            if (PART == 1) a.idx32[grow * a.k_top + pos] = ix[s];
-          }
-        }
+        ix[s] = kept[s] ? a.idx32[grow * a.k_top + pos] : 0;
       }
-      }  // PART != 2
-      if constexpr (PART == 1) {
-        MXA_PHASE(2);
-        continue;
-      }
-      if constexpr (PART == 2) {  // the kept indices of the selection kernel
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const int pos = 64 * s + lane;
-          kept[s] = pos < a.k_top;
-          ix[s] = kept[s] ? a.idx32[grow * a.k_top + pos] : 0;
-        }
-      }
-      MXA_PHASE(2);
       // ---- vals = true.gather(idx); softmax ----------------------------------
       float v[S];
       float mx = -INFINITY;
@@ -348,7 +280,7 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
         if (64 * s < a.k_top) {
           if (kept[s]) {
             bool nan = false;
-            v[s] = MXA_SKIP2(8) ? (float)(ix[s] & 3) : true_of(ix[s], nan);
+            v[s] = true_of(ix[s], nan);
             mx = fmaxf(mx, v[s]);
           }
         }
@@ -361,7 +293,6 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
         sum += v[s];
       }
       sum = wave_sum_f32(sum);
-      MXA_PHASE(3);
       // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -432,9 +363,8 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
       wave_lds_sync();
     }
 
-    MXA_PHASE(4);
     // ---- out = MX(P) @ MX(V): v_dot4 over 16 keys per read, fp64 block epilogue
-    if (!MXA_SKIP2(2)) {
+    {
       double acc[2] = {0.0, 0.0};
       bool nan[2] = {false, false};
       const int dsl = D > 64 ? 2 : 1;
@@ -482,9 +412,7 @@ __global__ __launch_bounds__(PART == 1 ? 256 : 1024, PART == 1 ? (BIG ? MXA_SELE
         if (64 * s < a.k_top && pos < a.k_top) prow[ix[s]] = 0;
       }
     }
-    MXA_PHASE(5);
   }
-  MXA_PHASE_FLUSH();
 }
 
 }  // namespace mxa

@@ -1,0 +1,366 @@
+// Exact-order top-k with ONE DPP ROW (16 lanes) PER ROW: four rows per wave.
+//
+// torch's CPU topk(k, largest, sorted) runs, per row of pair<double,int64>
+// (aten/src/ATen/native/TopKImpl.h:45-86, libstdc++ 11):
+//     k*64 <= n : std::partial_sort(begin, begin+k, end, cmp)
+//     else      : std::nth_element(begin, begin+k-1, end, cmp); std::sort(begin, begin+k-1, cmp)
+// and ties are the norm for the approximate scores, so the element
+// MOVEMENTS of __introselect / __introsort_loop / __unguarded_partition have to be
+// reproduced, not just the selected set.
+//
+// Each Hoare partition step is computed from stop flags and prefix counts (the rank
+// form derived in tools/topk_model.py and checked against libstdc++ by
+// tests/test_topk_model.py).  For pivot p at `first` (cmp = greater on order keys):
+//   left stop  x in (first, last): a[x] <= p      right stop y in (first, last): a[y] >= p
+//   (the pivot position never swaps and never counts)
+//   T(z) = left stops <= z + right stops <= z  (non-decreasing, +1 at least per position)
+//   cut  = first + 1 + #{z in (first,last) : T(z) <= totR}
+//   swaps: the left stops below the cut (nsw of them) trade places, in order, with the
+//   nsw highest right stops taken from the top.
+// Why this layout: the per-row work is a few prefix counts and a scatter, which a DPP
+// row does with row_shr scans and row_newbcast broadcasts (no SALU, no readlane);
+// the 16 lanes of a row hold E contiguous positions each (E = 2 .. 32, the narrowest
+// window that holds every pending range of the wave), so a step costs ~E
+// instructions per lane for FOUR rows at once instead of ~100+ per row for a
+// wave-wide step.  The row itself lives in an LDS mirror A (order key << 32 | index);
+// swaps publish their positions in P and then write their element to the partner's
+// position.
+//
+// std::sort's final insertion sort is a stable sort of the arrangement the introsort
+// loop leaves; because those segments are mutually ordered it equals a stable sort of
+// each <= 16-element segment (or of the whole prefix when k-1 <= 64), computed as a
+// stable rank.  Depth-limit heap fallbacks and partial_sort run serially on the
+// row's first lane (mxa_order.hpp, stl_heap.h semantics).
+#pragma once
+#include "mxa_order.hpp"
+
+namespace mxa {
+
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef __attribute__((address_space(3))) uint16_t lu16;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lu128;
+
+constexpr int kGStk = 24;  // pending introsort segments (>= depth limit 2*lg(511) + 1)
+constexpr int kGSeg = 16;  // final sort segments queued for one ranking pass
+
+// per-row LDS: mirror A[NP] (u64), exchange slots P[NP] + 16 trash slots (u16),
+// introsort stack, queue of final segments
+__host__ __device__ constexpr size_t grp_row_bytes(int NP) {
+  return (size_t)8 * NP + 2 * (NP + 16) + 4 * kGStk + 4 * kGSeg;
+}
+
+struct GrpRow {
+  lu64* A;
+  lu16* P;
+  lu32* stk;
+  lu32* seg;
+};
+__device__ __forceinline__ GrpRow carve_grp(unsigned char* base, int NP) {
+  GrpRow g;
+  g.A = (lu64*)(lu32*)(base);
+  g.P = (lu16*)(base + 8 * NP);
+  g.stk = (lu32*)(base + 10 * NP + 32);
+  g.seg = (lu32*)(base + 10 * NP + 32 + 4 * kGStk);
+  return g;
+}
+
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint32_t lowbits(int n) { return n >= 32 ? ~0u : ((1u << n) - 1u); }
+
+// acc * 2 + (a <= b): one compare and one add-with-carry (the compiler would emit a
+// compare, a select and an or)
+__device__ __forceinline__ uint32_t g_shl_le(uint32_t acc, uint32_t a, uint32_t b) {
+  asm("v_cmp_le_u32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+  return acc;
+}
+
+// DPP within each 16-lane row: row_shr with zero fill, row_newbcast:15
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t g_scan(uint32_t x) {  // inclusive prefix sum over the row
+  x += dpp_z<0x111>(x);
+  x += dpp_z<0x112>(x);
+  x += dpp_z<0x114>(x);
+  x += dpp_z<0x118>(x);
+  return x;
+}
+__device__ __forceinline__ uint32_t g_last(uint32_t x) {  // lane 15 of the row, to every lane of it
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x15F, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t g_sum(uint32_t x) { return g_last(g_scan(x)); }
+
+template <int E>
+constexpr int pow2_floor() { return E >= 32 ? 32 : E >= 16 ? 16 : E >= 8 ? 8 : E >= 4 ? 4 : E >= 2 ? 2 : 1; }
+
+// ---- one partition step ------------------------------------------------------
+// libstdc++ __unguarded_partition_pivot(first = f, last = l) (stl_algo.h: median of
+// (f+1, mid, l-1) moved to f, then __unguarded_partition of (f, l)) on every row of
+// the wave with act set (l - f >= 4), all rows in lockstep.  Window: lane gl holds
+// positions lb + e, lb = b + E*gl, e < E (b even, b <= f, l <= b + 16E <= NP).
+// HP = NP / 2 (> any swap count).  Returns the cut.
+template <int E, int HP>
+__device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
+  const int fa = act ? f : 0, la = act ? l : 4;  // idle rows read harmless positions
+  const int mid = fa + (la - fa) / 2;
+  const uint64_t xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1], xf = g.A[fa];
+  const uint32_t ka = hi32(xa), kb = hi32(xb), kc = hi32(xc);
+  // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free
+  const bool ab = ka > kb, bc = kb > kc, ac = ka > kc;
+  const int sel = ab ? (bc ? 1 : (ac ? 2 : 0)) : (ac ? 0 : (bc ? 2 : 1));
+  const int m = sel == 0 ? fa + 1 : (sel == 1 ? mid : la - 1);
+  const uint64_t xm = sel == 0 ? xa : (sel == 1 ? xb : xc);
+  const uint32_t p = hi32(xm);
+  if (act) {  // iter_swap(f, median)
+    g.A[f] = xm;
+    g.A[m] = xf;
+  }
+  wave_lds_sync();
+
+  const int lb = b + E * gl;
+  uint32_t K[E], I[E];
+#pragma unroll
+  for (int e = 0; e < E; e += 2) {
+    const u32x4 v = *(const lu128*)(g.A + lb + e);
+    I[e] = v.x;
+    K[e] = v.y;
+    I[e + 1] = v.z;
+    K[e + 1] = v.w;
+  }
+  // stop masks, bit (E-1-e) <-> position lb + e
+  uint32_t Lm = 0, Rm = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    Lm = g_shl_le(Lm, K[e], p);  // left stop:  !(a > p)
+    Rm = g_shl_le(Rm, p, K[e]);  // right stop: !(p > a)
+  }
+  const int lo = min(max(f + 1 - lb, 0), E), hi = min(max(l - lb, 0), E);
+  const uint32_t rng = act ? (lowbits(E - lo) & ~lowbits(E - hi)) : 0u;
+  Lm &= rng;
+  Rm &= rng;
+  const uint32_t cnt = (uint32_t)__popc(Lm) | ((uint32_t)__popc(Rm) << 16);
+  const uint32_t incl = g_scan(cnt);
+  const uint32_t tot = g_last(incl), excl = incl - cnt;
+  const uint32_t PL = excl & 0xFFFFu, PR = excl >> 16, PLR = PL + PR, totR = tot >> 16;
+  // cut = b + #{window positions z : T(z) <= totR}; per lane those are a prefix of
+  // its positions (T is non-decreasing), found by binary search on the prefix length
+  int j = 0;
+#pragma unroll
+  for (int st = pow2_floor<E>(); st >= 1; st >>= 1) {
+    const int c = j + st, sh = c <= E ? E - c : 0;
+    const bool ok = c <= E && PLR + (uint32_t)__popc(Lm >> sh) + (uint32_t)__popc(Rm >> sh) <= totR;
+    j = ok ? c : j;
+  }
+  const int cut = b + (int)g_sum((uint32_t)j);
+  // swapping left stops: the left stops below the cut (nsw of them); swapping right
+  // stops: the nsw highest, i.e. this lane's right stops after its first j0
+  const int cl = min(max(cut - lb, 0), E);
+  const uint32_t SLm = Lm & ~lowbits(E - cl);
+  const uint32_t nsw = g_sum((uint32_t)__popc(SLm));
+  const int j0 = min(max((int)(totR - nsw) - (int)PR, 0), E);
+  int c0 = 0;  // the longest prefix with fewer than j0 right stops: it ends at the j0-th
+#pragma unroll
+  for (int st = pow2_floor<E>(); st >= 1; st >>= 1) {
+    const int c = c0 + st, sh = c <= E ? E - c : 0;
+    const bool ok = c <= E && (int)__popc(Rm >> sh) < j0;
+    c0 = ok ? c : c0;
+  }
+  const int p0 = j0 == 0 ? 0 : min(c0 + 1, E);
+  const uint32_t SRm = Rm & lowbits(E - p0);
+  const uint32_t SW = SLm | SRm;
+  // the exchange: every swapping stop publishes its position in its slot (left: its
+  // rank among left stops; right: HP + its rank from the top); then each writes its
+  // element to the partner's position.  Non-swapping positions use the lane's trash
+  // slot and rewrite their own element (no exec-mask branches).
+  const uint32_t trash = 2 * HP + gl;
+  uint32_t slot[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int sh = E - 1 - e;
+    const uint32_t tl = PL + (uint32_t)__popc((Lm >> sh) >> 1);
+    const uint32_t tr = (uint32_t)HP + totR - PR - (uint32_t)__popc(Rm >> sh);
+    slot[e] = ((SW >> sh) & 1u) ? (((SLm >> sh) & 1u) ? tl : tr) : trash;
+    g.P[slot[e]] = (uint16_t)(lb + e);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const bool sw = (SW >> (E - 1 - e)) & 1u;
+    const uint32_t q = g.P[sw ? slot[e] ^ (uint32_t)HP : slot[e]];
+    g.A[sw ? (int)q : lb + e] = pack_ki(K[e], I[e]);
+  }
+  wave_lds_sync();
+  return cut;
+}
+
+// one partition of [f, l) on every row with act, in the narrowest window (16 E
+// positions from an even base at or below f) that holds every acting row's range
+template <int E, int NP>
+__device__ __forceinline__ bool grp_try(const GrpRow& g, int f, int l, bool act, int gl, int& cut) {
+  if (16 * E > NP) return false;
+  const int b = min(f & ~1, NP - 16 * E);
+  if (__builtin_amdgcn_ballot_w64(act && l - b > 16 * E) != 0) return false;
+  cut = grp_partition<E, NP / 2>(g, f, l, b, act, gl);
+  return true;
+}
+template <int NP>
+__device__ __forceinline__ int grp_partition_any(const GrpRow& g, int f, int l, bool act, int gl) {
+  int cut = 0;
+  if (grp_try<2, NP>(g, f, l, act, gl, cut) || grp_try<4, NP>(g, f, l, act, gl, cut) ||
+      grp_try<6, NP>(g, f, l, act, gl, cut) || grp_try<8, NP>(g, f, l, act, gl, cut) ||
+      grp_try<10, NP>(g, f, l, act, gl, cut) || grp_try<12, NP>(g, f, l, act, gl, cut) ||
+      grp_try<14, NP>(g, f, l, act, gl, cut) || grp_try<16, NP>(g, f, l, act, gl, cut) ||
+      grp_try<24, NP>(g, f, l, act, gl, cut))
+    return cut;
+  grp_try<32, NP>(g, f, l, act, gl, cut);
+  return cut;
+}
+
+// stable rank of [0, m) (m <= 16 EP): lane gl holds positions EP gl + e; a position's
+// rank counts the keys greater than its own and the equal keys before it
+template <int EP>
+__device__ __forceinline__ void grp_rank_prefix(const GrpRow& g, int m, bool valid, int gl) {
+  const int z0 = EP * gl;
+  uint32_t K[EP], I[EP], r[EP];
+#pragma unroll
+  for (int e = 0; e < EP; e += 2) {
+    const u32x4 v = *(const lu128*)(g.A + z0 + e);
+    I[e] = v.x;
+    K[e] = v.y;
+    I[e + 1] = v.z;
+    K[e + 1] = v.w;
+    r[e] = r[e + 1] = 0u;
+  }
+  for (int w = 0; w < m; ++w) {
+    const uint32_t kw = hi32(g.A[w]);
+#pragma unroll
+    for (int e = 0; e < EP; ++e) r[e] += (kw > K[e] || (kw == K[e] && w < z0 + e)) ? 1u : 0u;
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < EP; ++e)
+    if (valid && z0 + e < m) g.A[r[e]] = pack_ki(K[e], I[e]);
+}
+
+// stable rank of each queued segment (2..16 elements), one lane per segment
+__device__ __forceinline__ void grp_rank_segments(const GrpRow& g, int ns, int gl) {
+  if (gl < ns) {
+    const uint32_t sg = g.seg[gl];
+    const int f = (int)(sg & 0xFFFFu), len = (int)(sg >> 16) - f;
+    uint64_t x[16];
+    uint32_t r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      x[i] = i < len ? (uint64_t)g.A[f + i] : 0ull;  // key 0 sorts after every real key
+      r[i] = 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j < i) r[i] += hi32(x[j]) >= hi32(x[i]) ? 1u : 0u;
+        if (j > i) r[i] += hi32(x[j]) > hi32(x[i]) ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < len) g.A[f + r[i]] = x[i];
+  }
+}
+
+// ---- the whole top-k ----------------------------------------------------------
+// std::nth_element(begin, begin + k - 1, end) then std::sort(begin, begin + k - 1)
+// (or std::partial_sort when k*64 <= n) on every row of the wave.  One loop drives
+// both: each trip, every row settles its bookkeeping (exec-divergent, cheap) and then
+// every row with a pending range takes part in ONE partition step, so rows still in
+// the selection and rows already sorting share the wave's steps.  Afterwards g.A[p],
+// p < k, holds torch's p-th index in its low word.
+template <int NP>
+__device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool valid, int gl) {
+  if (k <= 0) return;
+  if (k * 64 <= n) {  // std::partial_sort(begin, begin + k, end)
+    if (valid && gl == 0) {
+      ln_heap_select(g.A, 0, k, n);
+      ln_sort_heap(g.A, 0, k);
+    }
+    wave_lds_sync();
+    return;
+  }
+  const int nth = k - 1, m = k - 1;
+  const bool queue = m > 64;  // final sort segments ranked one lane each (else the whole prefix)
+  int ph = valid ? 0 : 2;     // 0 __introselect, 1 __introsort_loop, 2 done
+  int f = 0, l = n, d = 2 * ilog2(n), sp = 0, ns = 0;
+  while (true) {
+    if (ph == 0 && (l - f <= 3 || d == 0)) {  // the selection ends
+      if (l - f > 3) {  // depth limit: __heap_select(f, nth + 1, l); iter_swap(f, nth)
+        if (gl == 0) {
+          ln_heap_select(g.A, f, nth + 1, l);
+          const uint64_t t = g.A[f];
+          g.A[f] = g.A[nth];
+          g.A[nth] = t;
+        }
+      } else if (l - f > 1 && gl == 0) {
+        ln_insertion_sort(g.A, f, l);  // __insertion_sort(f, l)
+      }
+      ph = m > 16 ? 1 : 2;
+      f = 0;
+      l = m;
+      d = m > 1 ? 2 * ilog2(m) : 0;
+    }
+    if (ph == 1) {
+      // settle: finished segments (<= 16 elements, or heap-sorted at the depth limit)
+      while (l - f <= 16 || d == 0) {
+        if (l - f > 16) {  // std::__partial_sort(f, l, l): heapsort, final as it stands
+          if (gl == 0) {
+            ln_heap_select(g.A, f, l, l);
+            ln_sort_heap(g.A, f, l);
+          }
+        } else if (queue && l - f >= 2) {
+          g.seg[ns] = (uint32_t)f | ((uint32_t)l << 16);
+          ++ns;
+          if (ns == kGSeg) {
+            wave_lds_sync();
+            grp_rank_segments(g, ns, gl);
+            ns = 0;
+          }
+        }
+        if (sp == 0) {
+          ph = 2;
+          break;
+        }
+        --sp;
+        const uint32_t e = g.stk[sp];
+        f = (int)(e & 1023u);
+        l = (int)((e >> 10) & 1023u);
+        d = (int)(e >> 20);
+      }
+    }
+    const bool act = ph < 2;
+    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+    wave_lds_sync();
+    const int cut = grp_partition_any<NP>(g, f, l, act, gl);
+    if (act) {
+      --d;
+      if (ph == 0) {
+        if (cut <= nth) f = cut;
+        else l = cut;
+      } else {
+        g.stk[sp] = (uint32_t)cut | ((uint32_t)l << 10) | ((uint32_t)d << 20);  // __introsort_loop(cut, l)
+        ++sp;
+        l = cut;
+      }
+    }
+  }
+  wave_lds_sync();
+  if (queue) {
+    if (valid && ns > 0) grp_rank_segments(g, ns, gl);
+  } else if (m >= 2) {
+    if (m <= 32) grp_rank_prefix<2>(g, m, valid, gl);
+    else grp_rank_prefix<4>(g, m, valid, gl);
+  }
+  wave_lds_sync();
+}
+
+}  // namespace mxa

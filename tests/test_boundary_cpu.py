@@ -46,9 +46,12 @@ def test_workspace_formula():
     from mx_quantization_amd import _native as N
     p = N.AttnParams()
     p.B, p.H, p.N, p.T, p.D = 256, 12, 197, 197, 64
+    p.top_k, p.approx, p.k_top, p.pred_mode = 1, 1, 20, 0
     nbytes = N.lib().mxa_attention_workspace_bytes(ctypes.byref(p))
-    # per head: Q,K codes + approx operands (4 x 197 x 64 B), P codes (197 x 224 B), V^T (64 x 224 B)
-    assert 3072 * (197 * (64 * 4 + 224) + 64 * 224) < nbytes < 3072 * 197 * 1000
+    # per head: Q,K codes + exponents + sign words (2 x 197 x (64 + 4 + 4 + 8) B),
+    # V^T codes + exponents (64 x 224 + 7 x 64 x 2 B), kept indices (197 x 20 x 4 B)
+    per_head = 2 * 197 * (64 + 4 + 4 + 8) + 64 * 224 + 7 * 64 * 2 + 197 * 20 * 4
+    assert 3072 * per_head <= nbytes < 3072 * per_head + 15 * 256
 
 
 def test_dropin_import_surface():
@@ -108,8 +111,8 @@ def _params(B, H, Nq, T, D, k, mode="ex_pred", top_k=1):
 
 
 def test_attention_path_selection_is_host_logic():
-    """mxa_attention_path: split row kernels for top-k at every bench shape, the
-    fused row kernel for the dense softmax or on request (no launch, no GPU)."""
+    """mxa_attention_path: selection + finishing kernels for top-k at every bench
+    shape, the dense row kernel for top_k=False (no launch, no GPU)."""
     import ctypes
     from mx_quantization_amd import _native as N
     lib = N.lib()
@@ -118,9 +121,5 @@ def test_attention_path_selection_is_host_logic():
         assert lib.mxa_attention_path(ctypes.byref(_params(*shape))) == split, shape
     assert lib.mxa_attention_path(ctypes.byref(_params(8, 16, 256, 120, 72, 20, "MXINT4"))) == split
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 3, 197, 197, 64, 20, top_k=0))) == fused
-    os.environ["MXA_ATTN_PATH"] = "fused"
-    try:
-        assert lib.mxa_attention_path(ctypes.byref(_params(256, 12, 197, 197, 64, 20))) == fused
-    finally:
-        os.environ.pop("MXA_ATTN_PATH")
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 600, 64, 5))) == -2  # T > 512
+    assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 60, 160, 5))) == -2  # D > 128

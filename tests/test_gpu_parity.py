@@ -110,16 +110,8 @@ def test_exponent_rule_exhaustive_sample(M):
 
 
 # ------------------------------------------------------------------ top-k order
-@pytest.fixture(params=["lane", "reg", "lds"])
-def impl(request):
-    """standalone top-k: lane-per-row tail (default for k <= 64), register-resident and LDS-resident rows"""
-    os.environ["MXA_TOPK_IMPL"] = request.param
-    yield request.param
-    os.environ.pop("MXA_TOPK_IMPL", None)
-
-
 @pytest.mark.parametrize("name", ["deit", "deit30", "dit", "cross"])
-def test_topk_ties_exact_order(M, impl, name):
+def test_topk_ties_exact_order(M, name):
     d = load("topk_ties.npz")
     k = int(d[f"{name}_k"])
     vals, idx = M.topk(dev(d[f"{name}_pred"]), k)
@@ -128,7 +120,7 @@ def test_topk_ties_exact_order(M, impl, name):
 
 
 @pytest.mark.parametrize("n", [120, 197, 256])
-def test_topk_adversarial_rows(M, impl, n):
+def test_topk_adversarial_rows(M, n):
     d = load("topk_ties.npz")
     rows, ks, want = d[f"adv{n}_rows"], d[f"adv{n}_k"], d[f"adv{n}_idx"]
     for k in np.unique(ks):
@@ -138,7 +130,7 @@ def test_topk_adversarial_rows(M, impl, n):
 
 
 @pytest.mark.parametrize("n,k", [(197, 30), (197, 154), (256, 77), (256, 154), (512, 300), (120, 20), (300, 4)])
-def test_topk_depth_limit_fallbacks_and_partial_sort(M, impl, n, k):
+def test_topk_depth_limit_fallbacks_and_partial_sort(M, n, k):
     rows = np.stack([O.antiqsort_row(n, k)] + [np.random.default_rng(i).integers(0, 3, n).astype(np.float32)
                                                 for i in range(7)])
     _, want = O.topk(rows, k)
@@ -146,7 +138,7 @@ def test_topk_depth_limit_fallbacks_and_partial_sort(M, impl, n, k):
     same(host(idx), want, f"n{n} k{k}")
 
 
-def test_topk_random_small_alphabets_and_specials(M, impl):
+def test_topk_random_small_alphabets_and_specials(M):
     rng = np.random.default_rng(11)
     for n in (5, 17, 64, 65, 127, 128, 129, 197, 256, 300, 511, 512):
         for k in sorted({1, 2, 3, min(n, 20), (n + 1) // 2, n}):
@@ -159,8 +151,9 @@ def test_topk_random_small_alphabets_and_specials(M, impl):
 
 
 @pytest.mark.parametrize("n", [33, 64, 65, 100, 197, 256, 512])
-def test_topk_lane_tail_many_rows(M, n):
-    """the lane-per-row tail (windows W = 32 and 64) on thousands of rows with heavy ties"""
+def test_topk_many_tie_rows(M, n):
+    """thousands of rows with heavy ties: every window width of the group partition
+    steps (4, 8, 16, 32 positions per lane), both sort-rank paths (k-1 <= 64 and > 64)"""
     rng = np.random.default_rng(n)
     for k in sorted({1, 2, 5, 16, 17, 20, 30, 32, 33, 48, 64} & set(range(1, n + 1))):
         rows = rng.integers(-6, 7, (700, n)).astype(np.float32) * np.float32(0.25)
@@ -259,23 +252,13 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
         assert O.normwise_rel_err(host(out[b:b + 1]), r["out"]) <= OUT_TOL
 
 
-PATHS = ("rows", "fused", "rows1", "tiles")
+PATHS = ("split",)
 
 
 def _attn_all_paths(M, q, k, v, scale, **kw):
-    """Run the op on every kernel path: the split row kernels v2 (selection kernel +
-    finishing kernel, the default for top-k), the one fused row kernel v2
-    (MXA_ATTN_PATH=fused), the v1 row kernel + pv_kernel (rows1) and the MFMA
-    score-tile kernel (tiles)."""
-    res = []
-    for path in (None, "fused", "rows1", "tiles"):
-        if path:
-            os.environ["MXA_ATTN_PATH"] = path
-        try:
-            res.append(M.mx_topk_attention(dev(q), dev(k), dev(v), scale, return_scores=True, **kw))
-            torch.cuda.synchronize()
-        finally:
-            os.environ.pop("MXA_ATTN_PATH", None)
+    """Run the op (selection kernel + finishing kernel for top-k)."""
+    res = [M.mx_topk_attention(dev(q), dev(k), dev(v), scale, return_scores=True, **kw)]
+    torch.cuda.synchronize()
     return [[host(t) for t in r] for r in res]
 
 
@@ -292,9 +275,9 @@ def _check_vs_oracle(got, r, what):
 
 @pytest.mark.parametrize("D", [32, 64, 72, 128])
 @pytest.mark.parametrize("N,T,k", [(197, 197, 20), (256, 256, 154), (5, 64, 7), (1, 20, 5), (70, 130, 65)])
-def test_expred_rows_and_tiles_paths_vs_oracle(M, D, N, T, k):
-    """Both fused kernels against the oracle over head dims of 1..4 MX blocks,
-    short and long rows, k in both top-k branches."""
+def test_expred_paths_vs_oracle(M, D, N, T, k):
+    """The op against the oracle over head dims of 1..4 MX blocks, short and long
+    rows, k in both top-k branches."""
     rng = np.random.default_rng(D * 1000 + N)
     B, H = 2, 3
     q = rng.standard_normal((B, H, N, D), dtype=np.float32)
@@ -343,26 +326,6 @@ def test_approx_modes_all_paths_vs_oracle(M, mode, N, T, k):
     r = O.attention(q, kk, v, 72 ** -0.5, k_top=k, pred_mode=mode)
     for got, name in zip(outs, PATHS):
         _check_vs_oracle(got, r, name)
-
-
-@pytest.mark.parametrize("D,N,T,k,mode", [(64, 197, 197, 20, "ex_pred"), (72, 256, 256, 154, "ex_pred"),
-                                          (72, 77, 120, 20, "MXINT4"), (72, 33, 120, 77, "two_step_leading_ones")])
-def test_finish_mfma_kernel_vs_oracle(M, D, N, T, k, mode):
-    """The int8-MFMA finishing kernel (MXA_FINISH=mfma: P.V over 16-row tiles, one
-    v_mfma_i32_16x16x32_i8 per 32-key MX block, fp64 block epilogue), partial tiles."""
-    rng = np.random.default_rng(13)
-    B, H = 1, 3
-    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
-    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
-    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
-    os.environ["MXA_FINISH"] = "mfma"
-    try:
-        got = M.mx_topk_attention(dev(q), dev(kk), dev(v), D ** -0.5, k_top=k, pred_mode=mode, return_scores=True)
-        torch.cuda.synchronize()
-    finally:
-        os.environ.pop("MXA_FINISH", None)
-    r = O.attention(q, kk, v, D ** -0.5, k_top=k, pred_mode=mode)
-    _check_vs_oracle([host(t) for t in got], r, "finish_mfma")
 
 
 def test_pixart_cross_full_batch(M):

@@ -6,7 +6,7 @@ import sys
 
 pat = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(pat)):
+for f in sorted(glob.glob(pat, recursive=True)):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"][:48]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in agg.items():
