@@ -185,9 +185,13 @@ int mxa_matmul(const float* a, const float* b, float* c, int64_t batch, int32_t 
                int64_t workspace_bytes, hipStream_t stream);
 int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc);
 
-/* Self-test of the int8 MFMA operand/accumulator lane maps (16x16x32): writes
- * C = A(16x32) * B(32x16) computed by MFMA and returns MXA_OK; host compares. */
+/* Self-tests of the int8 MFMA operand/accumulator lane maps the kernels rely on:
+ * C = A * B computed by one MFMA, row-major int8 operands, int32 result; the host
+ * compares.  mxa_selftest_mfma: v_mfma_i32_16x16x32_i8 (A 16x32, B 32x16; mx.matmul);
+ * mxa_selftest_mfma32: v_mfma_i32_32x32x32_i8 (A 32x32, B 32x32; the finishing
+ * kernel's P.V). */
 int mxa_selftest_mfma(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream);
+int mxa_selftest_mfma32(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream);
 
 #ifdef __cplusplus
 }

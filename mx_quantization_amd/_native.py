@@ -58,6 +58,7 @@ _SIGS = {
                            c_vp, c_i64, c_vp]),
     "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
     "mxa_selftest_mfma": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
+    "mxa_selftest_mfma32": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -5,8 +5,9 @@
 //   cols_prep(V)                MXINT8 codes of V along tokens, stored [d][t]
 //   select_kernel               approximate scores + torch-CPU-order top-k, four query
 //                               rows per wave (mxa_select.hpp, mxa_topk_grp.hpp)
-//   attn_rows2_kernel<..., 2>   the kept keys' true scores, softmax, MX(P), P.V
-//                               (mxa_rows2.hpp); <..., 0> the dense (top_k=False) branch
+//   finish_kernel               the kept keys' true scores, softmax, MX(P), P.V on int8
+//                               MFMA (mxa_finish.hpp)
+//   attn_rows2_kernel<..., 0>   the dense (top_k=False) branch (mxa_rows2.hpp)
 //
 // This is the mx_quant branch of the patched attention forward:
 //   workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
@@ -39,7 +40,7 @@ __device__ __forceinline__ int s_exp16(const int16_t* base, int64_t i) {
 }  // namespace mxa
 
 #include "mxa_rows2.hpp"
-#include "mxa_select.hpp"
+#include "mxa_finish.hpp"
 
 namespace mxa {
 
@@ -200,7 +201,7 @@ static int launch_rows2_p(const Rows2Args& ra0, int BH, hipStream_t stream) {
 template <int NP, int MODE>
 static size_t select_lds(const Rows2Args& ra) {
   return rows2_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, 1, ra.tpad, 0, 0, 1).waves +
-         (size_t)4 * kSelWaves * grp_row_bytes(NP);
+         (size_t)4 * kSelWaves * grp_row_bytes(grp_alloc(ra.T), NP);
 }
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
@@ -234,25 +235,67 @@ static int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stre
   }
 }
 
+// ---- finishing kernel (mxa_finish.hpp): 32-row MFMA tiles, one per wave ------------
+static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg) {
+  const int tiles = (ra.N + kFinTile - 1) / kFinTile;
+  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w).total; };
+  if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  // a head's tiles over the waves of one workgroup (the K / V tables staged once);
+  // few heads (PixArt cross-attention): split the tiles over grid.y so that the grid
+  // still has ~2 workgroups per CU
+  int chunks = 1;
+  while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
+  int w = std::min(8, (tiles + chunks - 1) / chunks);
+  while (w > 1 && lds(w) > 160 * 1024) --w;
+  *waves = w;
+  *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
+  return MXA_OK;
+}
+template <int KS>
+static int launch_finish_ks(const Rows2Args& ra0, int BH, hipStream_t stream) {
+  Rows2Args ra = ra0;
+  int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
+  if (rc) return rc;
+  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<KS>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL((finish_kernel<KS>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (plan) {
+    int w, r;
+    return finish_plan(ra, BH, &w, &r);
+  }
+  const int ks = (ra.k_top + 15) / 16;
+  if (ks <= 1) return launch_finish_ks<1>(ra, BH, stream);
+  if (ks <= 2) return launch_finish_ks<2>(ra, BH, stream);
+  if (ks <= 4) return launch_finish_ks<4>(ra, BH, stream);
+  if (ks <= 8) return launch_finish_ks<8>(ra, BH, stream);
+  if (ks <= 16) return launch_finish_ks<16>(ra, BH, stream);
+  return launch_finish_ks<32>(ra, BH, stream);
+}
+
 // the row kernel of the path: the finishing kernel (top-k) or the dense kernel
 template <int S>
-static int launch_rows_s(const Rows2Args& ra, bool topk, bool true_mode, int BH, hipStream_t stream, bool plan) {
-  if (plan) {  // feasibility only
-    const int mode = topk && !true_mode ? kModeExSign : kModeTrue;
-    return rows2_waves(mode, ra, S, topk ? 2 : 0) > 0 ? MXA_OK : MXA_ERR_UNSUPPORTED;
-  }
-  if (!topk) return launch_rows2_p<S, kModeTrue, false, 0>(ra, BH, stream);
-  // MODE only decides whether the finishing kernel writes the true-score debug output
-  // (the selection kernel already did when it ranked the true scores)
-  if (true_mode) return launch_rows2_p<S, kModeTrue, true, 2>(ra, BH, stream);
-  return launch_rows2_p<S, kModeExSign, true, 2>(ra, BH, stream);
+static int launch_rows_s(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (plan) return rows2_waves(kModeTrue, ra, S, 0) > 0 ? MXA_OK : MXA_ERR_UNSUPPORTED;  // feasibility only
+  return launch_rows2_p<S, kModeTrue, false, 0>(ra, BH, stream);
 }
 static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan) {
+  if (topk) {
+    // the selection kernel already wrote the true scores when it ranked them
+    Rows2Args rf = ra;
+    if (true_mode) rf.true_out = nullptr;
+    return launch_finish(rf, BH, stream, plan);
+  }
   switch (S) {
-    case 1: return launch_rows_s<1>(ra, topk, true_mode, BH, stream, plan);
-    case 2: return launch_rows_s<2>(ra, topk, true_mode, BH, stream, plan);
-    case 4: return launch_rows_s<4>(ra, topk, true_mode, BH, stream, plan);
-    default: return launch_rows_s<8>(ra, topk, true_mode, BH, stream, plan);
+    case 1: return launch_rows_s<1>(ra, BH, stream, plan);
+    case 2: return launch_rows_s<2>(ra, BH, stream, plan);
+    case 4: return launch_rows_s<4>(ra, BH, stream, plan);
+    default: return launch_rows_s<8>(ra, BH, stream, plan);
   }
 }
 
@@ -405,7 +448,7 @@ extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream,
 // ---- standalone top-k: one DPP row per row (mxa_topk_grp.hpp) -----------------------
 template <int NP>
 static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t stream) {
-  const size_t lds = (size_t)16 * grp_row_bytes(NP);
+  const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_grp_kernel<NP>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
@@ -467,6 +510,12 @@ extern "C" int mxa_matmul(const float* a, const float* b, float* c, int64_t batc
   MatmulArgs ma{ac, as, bt, bsc, M, Nc, nbk, kpad, bfloat, c};
   dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 15) / 16), (unsigned)batch);
   hipLaunchKernelGGL(matmul_kernel, grid, dim3(256), 0, stream, ma);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_selftest_mfma32(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream) {
+  if (!a || !b || !c) return MXA_ERR_ARG;
+  hipLaunchKernelGGL(selftest_mfma32_kernel, dim3(1), dim3(64), 0, stream, a, b, c);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 

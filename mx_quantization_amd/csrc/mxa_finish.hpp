@@ -1,0 +1,253 @@
+// Finishing kernel of the top-k path: for every query row and its k kept keys
+// (select_kernel's indices), the true scores, softmax, MX(P) along keys and P.V,
+// with P.V on int8 MFMA.
+//
+// Per workgroup (one head, or a chunk of its query rows when there are few heads):
+// the head's K codes + exponents and V^T codes + exponents are staged in LDS once.
+// Per wave, tiles of 32 query rows:
+//   1. eight passes of four rows, one 16-lane DPP row per query row (the layout of
+//      select_kernel): lane gl takes kept slots gl, gl+16, ...; the kept key's true
+//      score fl32(exact sum) * scale (+ bias) by v_dot4 over the LDS codes with an
+//      exact fp64 block epilogue; softmax over the kept scores (DPP
+//      row reductions); P MX-quantized along keys (block maxima by LDS atomic max)
+//      into the tile's dense code rows in LDS (zero elsewhere), block scales as
+//      floats (NaN for a NaN block);
+//   2. P.V for the tile: per 32 output columns and per 32-key MX block ONE
+//      v_mfma_i32_32x32x32_i8 (K = 32 = one block, so each block keeps its exact
+//      int32 sum), epilogue acc += C * (sP[row][b] * sV[b][d]) in fp32 (P.V is a
+//      tolerance-only product);
+//   3. the tile's output rows are written as 128-B row segments and its code rows
+//      are cleared for the next tile.
+// Reference: microxscaling/mx/matmul.py:68-76 (MX P.V), callers
+// workloads/deit/scripts/main.py:124-152, workloads/DiT/models.py:195-225,
+// workloads/PixArt/models/MX_transformer_block.py:679-717, :826-859.
+#pragma once
+#include "mxa_select.hpp"
+
+namespace mxa {
+
+constexpr int kFinTile = 32;  // query rows per MFMA tile (one wave)
+
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef int v4i_ __attribute__((ext_vector_type(4)));
+
+// LDS layout: tables, then per wave the P code tile [32][vst], the P block scales
+// sP [ntb][32] (float), the block maxima bm [4][16] (u32, one DPP row each)
+struct FinLds {
+  size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
+};
+__host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves) {
+  FinLds L;
+  size_t o = 0;
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  L.kc = o;
+  o += al((size_t)T * kst);
+  L.ke = o;
+  o += al((size_t)T * nbd * 2);
+  L.vt = o;
+  o += al((size_t)D * vst);
+  L.ve = o;
+  o += al((size_t)ntb * D * 2);
+  L.waves = o;
+  L.sp = al((size_t)kFinTile * vst);
+  L.bm = L.sp + al((size_t)ntb * kFinTile * 4);
+  L.per_wave = L.bm + 4 * 16 * 4;
+  L.total = o + (size_t)waves * L.per_wave;
+  return L;
+}
+
+// exact 2^e as float (subnormal below -126, 0 below -149); NaN for the NaN exponent
+__device__ __forceinline__ float scale_f(int e) {
+  return e == kExpNaN ? __uint_as_float(0x7FC00000u) : (e < -149 ? 0.0f : pow2f(e));
+}
+
+// KS: kept slots per lane (k <= 16 KS)
+template <int KS>
+__global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
+  const int bh = blockIdx.x;
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
+  const int b_ = bh / a.H, h_ = bh % a.H;
+  const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves);
+  int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
+  int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
+  int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
+  int16_t* tve = reinterpret_cast<int16_t*>(smem + L.ve);
+  unsigned char* wb = smem + L.waves + (size_t)wave * L.per_wave;
+  int8_t* ptile = reinterpret_cast<int8_t*>(wb);
+  float* sP = reinterpret_cast<float*>(wb + L.sp);
+  uint32_t* bm = reinterpret_cast<uint32_t*>(wb + L.bm) + 16 * gi;
+
+  // ---- stage the head's K and V tables; clear the code tile -----------------------
+  const int64_t kb = (int64_t)bh * T;
+  {
+    const int cpr = a.dpad / 16;
+    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+      const int j = i / cpr, c = i - j * cpr;
+      *reinterpret_cast<uint4*>(tkc + (size_t)j * kst + 16 * c) =
+          *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
+    }
+    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tke[i] = a.ksT[kb * nbd + i];
+    const int vpr = a.tpad / 16;
+    const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
+    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
+      const int d = i / vpr, c = i - d * vpr;
+      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
+          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+    }
+    const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
+    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tve[i] = vssrc[i];
+    for (int i = lane; i < kFinTile * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
+    bm[gl] = 0u;
+  }
+  __syncthreads();
+
+  const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
+  for (int r0 = r_beg + kFinTile * wave; r0 < r_end; r0 += kFinTile * a.waves) {
+    // ---- 1. kept scores, softmax, MX(P) into the code tile: four rows per pass ----
+    for (int pass = 0; pass < kFinTile / 4; ++pass) {
+      const int tr = 4 * pass + gi;  // row within the tile
+      const int r = r0 + tr;
+      const bool valid = r < r_end;
+      const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
+      const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
+      const int8_t* qsrc = a.qc + grow * a.dpad;
+      uint4 qv[2 * kMaxNB];
+      int qe[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) {
+        qv[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b) : make_uint4(0, 0, 0, 0);
+        qv[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
+        qe[b] = b < nbd ? exp_from16(a.qsT[grow * nbd + b]) : 0;
+      }
+      auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
+        bool nan = false;
+        const double acc = g_dot<0>(qv, qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
+        float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
+        if (brow) t = t + brow[(int64_t)j * a.bs3];
+        return t;
+      };
+      if (a.true_out && valid)  // debug output: every key's true score
+        for (int j = gl; j < T; j += 16) a.true_out[grow * T + j] = true_of(j);
+
+      int ix[KS];
+      float v[KS];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        const int s = gl + 16 * t;
+        const bool kept = valid && s < k;
+        ix[t] = kept ? a.idx32[grow * k + s] : -1;
+        v[t] = kept ? true_of(ix[t]) : -INFINITY;
+        mx = fmaxf(mx, v[t]);
+      }
+      mx = __uint_as_float(row16_reduce(__float_as_uint(mx), [](uint32_t x, uint32_t y) {
+        return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
+      }));
+      float sum = 0.0f;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        v[t] = ix[t] >= 0 ? expf(v[t] - mx) : 0.0f;
+        sum += v[t];
+      }
+      sum = __uint_as_float(row16_reduce(__float_as_uint(sum), [](uint32_t x, uint32_t y) {
+        return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
+      }));
+      // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        if (ix[t] >= 0) {
+          v[t] = round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1);
+          atomicMax(&bm[ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
+        }
+      }
+      wave_lds_sync();
+      if (gl < ntb) {  // block gl: scale exponent (+1024; 0 = NaN block) and flush flag
+        int e_raw;
+        const int es = scale_exponent(bm[gl], 127, &e_raw);
+        const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
+        sP[gl * kFinTile + tr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
+        bm[gl] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        if (ix[t] >= 0) {
+          const uint32_t e = bm[ix[t] >> 5];
+          int code = 0;
+          if (e & 0xFFFFu) {
+            const int es = (int)(e & 0xFFFFu) - 1024;
+            const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
+            code = (int)round_code(x, es, 8, kRoundNearest);
+          }
+          ptile[tr * vst + ix[t]] = (int8_t)code;
+        }
+      }
+      wave_lds_sync();
+      bm[gl] = 0u;
+    }
+    wave_lds_sync();
+
+    // ---- 2. P.V on int8 MFMA: one v_mfma_i32_32x32x32_i8 per (32 columns, key block) ----
+    // lane maps (checked on hardware by mxa_selftest_mfma32): A[m][k], m = lane % 32,
+    // k = 16 (lane / 32) + 0..15; B[k][n], n = lane % 32, the same k; C[m][n] in c[i],
+    // m = 8 (i / 4) + 4 (lane / 32) + i % 4, n = lane % 32
+    const int m0 = 4 * (lane >> 5), ln = lane & 31, kh = 16 * (lane >> 5);
+    for (int dt = 0; dt < D; dt += 32) {
+      const int d = min(dt + ln, D - 1);
+      float acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+      for (int b = 0; b < ntb; ++b) {
+        const v4i_ av = *reinterpret_cast<const v4i_*>(ptile + ln * vst + 32 * b + kh);
+        const v4i_ bv = *reinterpret_cast<const v4i_*>(tvt + (size_t)d * vst + 32 * b + kh);
+        const v16i zero = {};
+        const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
+        const float sv = scale_f(exp_from16(tve[b * D + d]));
+        const float* sp = sP + b * kFinTile;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 s4 = *reinterpret_cast<const float4*>(sp + 8 * q + m0);
+          acc[4 * q + 0] = fmaf((float)c[4 * q + 0], s4.x * sv, acc[4 * q + 0]);
+          acc[4 * q + 1] = fmaf((float)c[4 * q + 1], s4.y * sv, acc[4 * q + 1]);
+          acc[4 * q + 2] = fmaf((float)c[4 * q + 2], s4.z * sv, acc[4 * q + 2]);
+          acc[4 * q + 3] = fmaf((float)c[4 * q + 3], s4.w * sv, acc[4 * q + 3]);
+        }
+      }
+      // ---- 3. output rows (128-B segments per row) --------------------------------
+      if (dt + ln < D) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = r0 + 8 * (i >> 2) + m0 + (i & 3);
+          if (r < r_end)
+            a.out[b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + dt + ln] = round_bfloat(acc[i], a.bfloat, kRoundNearest, 1);
+        }
+      }
+    }
+    wave_lds_sync();
+    for (int i = lane; i < kFinTile * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
+    wave_lds_sync();
+  }
+}
+
+// Self-test of the v_mfma_i32_32x32x32_i8 lane maps used above: A (32x32 row-major
+// M x K), B (32x32 row-major K x N) -> C (32x32 row-major) through the same maps.
+__global__ void selftest_mfma32_kernel(const int8_t* A, const int8_t* B, int32_t* C) {
+  const int lane = threadIdx.x, ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
+  v4i_ a4, b4;
+  for (int w = 0; w < 4; ++w) {
+    uint32_t x = 0, y = 0;
+    for (int j = 0; j < 4; ++j) {
+      x |= (uint32_t)(uint8_t)A[ln * 32 + kh + 4 * w + j] << (8 * j);
+      y |= (uint32_t)(uint8_t)B[(kh + 4 * w + j) * 32 + ln] << (8 * j);
+    }
+    a4[w] = (int)x;
+    b4[w] = (int)y;
+  }
+  const v16i zero = {};
+  const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a4, b4, zero, 0, 0, 0);
+  for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + m0 + (i & 3)) * 32 + ln] = c[i];
+}
+
+}  // namespace mxa

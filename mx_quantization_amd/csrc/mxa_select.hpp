@@ -53,7 +53,7 @@ __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd,
 }
 
 template <int NP, int MODE>
-__global__ __launch_bounds__(64 * kSelWaves) void select_kernel(Rows2Args a) {
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
@@ -85,7 +85,8 @@ __global__ __launch_bounds__(64 * kSelWaves) void select_kernel(Rows2Args a) {
   }
   __syncthreads();
 
-  const GrpRow g = carve_grp(smem + L.waves + (size_t)(4 * wave + gi) * grp_row_bytes(NP), NP);
+  const int npa = grp_alloc(T);
+  const GrpRow g = carve_grp(smem + L.waves + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
   const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
   for (int rq = (int)blockIdx.y * a.rows_per_wg + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
     const int r = rq + gi;
@@ -175,12 +176,13 @@ struct GrpTopkArgs {
 };
 
 template <int NP>
-__global__ __launch_bounds__(256) void topk_grp_kernel(GrpTopkArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void topk_grp_kernel(GrpTopkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
   const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * 4 + gi;
   const bool valid = row < a.rows;
-  const GrpRow g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(NP), NP);
+  const int npa = grp_alloc(a.n);
+  const GrpRow g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
   const float* src = a.vals + (valid ? row : 0) * a.ld;
   if (valid)
     for (int j = gl; j < a.n; j += 16) g.A[j] = pack_ki(order_key(src[j]), (uint32_t)j);

@@ -38,31 +38,51 @@ namespace mxa {
 
 typedef __attribute__((address_space(3))) uint32_t lu32;
 typedef __attribute__((address_space(3))) uint16_t lu16;
+typedef __attribute__((address_space(3))) uint8_t lu8;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lu128;
 
 constexpr int kGStk = 24;  // pending introsort segments (>= depth limit 2*lg(511) + 1)
 constexpr int kGSeg = 16;  // final sort segments queued for one ranking pass
 
-// per-row LDS: mirror A[NP] (u64), exchange slots P[NP] + 16 trash slots (u16),
-// introsort stack, queue of final segments
-__host__ __device__ constexpr size_t grp_row_bytes(int NP) {
-  return (size_t)8 * NP + 2 * (NP + 16) + 4 * kGStk + 4 * kGSeg;
+// Row capacity: NP (128, 256 or 512, a template parameter: the exchange slots'
+// width and the swap-rank split HP = NP/2) and the mirror's allocated positions NPA
+// (runtime: T rounded up to a window width, so that the LDS per row -- and with it
+// the resident waves -- follows the row length)
+// per-row LDS: mirror A[NPA] (u64), exchange slots P[NP] + 16 trash slots (u8 for
+// NP <= 256, else u16), introsort stack, queue of final segments
+__host__ __device__ constexpr int grp_pbytes(int NP) { return ((NP <= 256 ? 1 : 2) * (NP + 16) + 15) & ~15; }
+__host__ __device__ constexpr size_t grp_row_bytes(int NPA, int NP) {
+  return (size_t)8 * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg;
 }
+// (the window widths 16 E are 32, 64, ..., 256, 384, 512, so NPA is one of them)
+__host__ __device__ constexpr int grp_alloc(int T) { return T <= 256 ? (T + 31) & ~31 : (T <= 384 ? 384 : 512); }
 
 struct GrpRow {
   lu64* A;
-  lu16* P;
+  unsigned char __attribute__((address_space(3)))* P;
   lu32* stk;
   lu32* seg;
+  int npa;  // allocated mirror positions
 };
-__device__ __forceinline__ GrpRow carve_grp(unsigned char* base, int NP) {
+__device__ __forceinline__ GrpRow carve_grp(unsigned char* base, int npa, int NP) {
   GrpRow g;
   g.A = (lu64*)(lu32*)(base);
-  g.P = (lu16*)(base + 8 * NP);
-  g.stk = (lu32*)(base + 10 * NP + 32);
-  g.seg = (lu32*)(base + 10 * NP + 32 + 4 * kGStk);
+  g.P = (unsigned char __attribute__((address_space(3)))*)(base + 8 * npa);
+  g.stk = (lu32*)(base + 8 * npa + grp_pbytes(NP));
+  g.seg = (lu32*)(base + 8 * npa + grp_pbytes(NP) + 4 * kGStk);
+  g.npa = npa;
   return g;
+}
+template <int NP>
+__device__ __forceinline__ void p_put(const GrpRow& g, uint32_t i, uint32_t v) {
+  if constexpr (NP <= 256) ((lu8*)g.P)[i] = (uint8_t)v;
+  else ((lu16*)g.P)[i] = (uint16_t)v;
+}
+template <int NP>
+__device__ __forceinline__ uint32_t p_get(const GrpRow& g, uint32_t i) {
+  if constexpr (NP <= 256) return ((lu8*)g.P)[i];
+  else return ((lu16*)g.P)[i];
 }
 
 __device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
@@ -99,10 +119,11 @@ constexpr int pow2_floor() { return E >= 32 ? 32 : E >= 16 ? 16 : E >= 8 ? 8 : E
 // libstdc++ __unguarded_partition_pivot(first = f, last = l) (stl_algo.h: median of
 // (f+1, mid, l-1) moved to f, then __unguarded_partition of (f, l)) on every row of
 // the wave with act set (l - f >= 4), all rows in lockstep.  Window: lane gl holds
-// positions lb + e, lb = b + E*gl, e < E (b even, b <= f, l <= b + 16E <= NP).
+// positions lb + e, lb = b + E*gl, e < E (b even, b <= f, l <= b + 16E <= NPA).
 // HP = NP / 2 (> any swap count).  Returns the cut.
-template <int E, int HP>
+template <int E, int NP>
 __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
+  constexpr int HP = NP / 2;
   const int fa = act ? f : 0, la = act ? l : 4;  // idle rows read harmless positions
   const int mid = fa + (la - fa) / 2;
   const uint64_t xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1], xf = g.A[fa];
@@ -182,13 +203,13 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
     const uint32_t tl = PL + (uint32_t)__popc((Lm >> sh) >> 1);
     const uint32_t tr = (uint32_t)HP + totR - PR - (uint32_t)__popc(Rm >> sh);
     slot[e] = ((SW >> sh) & 1u) ? (((SLm >> sh) & 1u) ? tl : tr) : trash;
-    g.P[slot[e]] = (uint16_t)(lb + e);
+    p_put<NP>(g, slot[e], (uint32_t)(lb + e));
   }
   wave_lds_sync();
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const bool sw = (SW >> (E - 1 - e)) & 1u;
-    const uint32_t q = g.P[sw ? slot[e] ^ (uint32_t)HP : slot[e]];
+    const uint32_t q = p_get<NP>(g, sw ? slot[e] ^ (uint32_t)HP : slot[e]);
     g.A[sw ? (int)q : lb + e] = pack_ki(K[e], I[e]);
   }
   wave_lds_sync();
@@ -199,10 +220,10 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
 // positions from an even base at or below f) that holds every acting row's range
 template <int E, int NP>
 __device__ __forceinline__ bool grp_try(const GrpRow& g, int f, int l, bool act, int gl, int& cut) {
-  if (16 * E > NP) return false;
-  const int b = min(f & ~1, NP - 16 * E);
+  if (16 * E > NP || 16 * E > g.npa) return false;
+  const int b = min(f & ~1, g.npa - 16 * E);
   if (__builtin_amdgcn_ballot_w64(act && l - b > 16 * E) != 0) return false;
-  cut = grp_partition<E, NP / 2>(g, f, l, b, act, gl);
+  cut = grp_partition<E, NP>(g, f, l, b, act, gl);
   return true;
 }
 template <int NP>

@@ -234,3 +234,13 @@ def selftest_mfma(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     check(lib().mxa_selftest_mfma(a.contiguous().data_ptr(), b.contiguous().data_ptr(), c.data_ptr(),
                                   stream_ptr(dev)), "mxa_selftest_mfma")
     return c
+
+
+def selftest_mfma32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """C = A (32x32 int8) @ B (32x32 int8) by one v_mfma_i32_32x32x32_i8 through the
+    finishing kernel's lane maps."""
+    dev = require_device(a, b)
+    c = torch.empty((32, 32), dtype=torch.int32, device=dev)
+    check(lib().mxa_selftest_mfma32(a.contiguous().data_ptr(), b.contiguous().data_ptr(), c.data_ptr(),
+                                    stream_ptr(dev)), "mxa_selftest_mfma32")
+    return c

@@ -60,6 +60,17 @@ def test_mfma_i8_lane_maps(M):
     same(C, A.astype(np.int32) @ B.astype(np.int32), "mfma 16x16x32 i8")
 
 
+def test_mfma_i8_32x32x32_lane_maps(M):
+    """the finishing kernel's P.V operand / accumulator maps (v_mfma_i32_32x32x32_i8)"""
+    from mx_quantization_amd.ops import selftest_mfma32
+    rng = np.random.default_rng(1)
+    for lo, hi in ((-128, 128), (-127, 128), (0, 2)):
+        A = rng.integers(lo, hi, (32, 32)).astype(np.int8)
+        B = rng.integers(lo, hi, (32, 32)).astype(np.int8)
+        C = host(selftest_mfma32(dev(A), dev(B)))
+        same(C, A.astype(np.int32) @ B.astype(np.int32), "mfma 32x32x32 i8")
+
+
 # ------------------------------------------------------------------ quantization
 @pytest.mark.parametrize("elem,mbits", [("int8", 8), ("int4", 4), ("int2", 2)])
 @pytest.mark.parametrize("rnd", ["nearest", "floor", "even"])

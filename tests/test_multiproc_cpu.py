@@ -1,8 +1,12 @@
-"""Multi-process path of bench.py on CPU (gloo, world_size 2): each rank builds
-its own shard of images (weak scaling, no data-path collective), the timed region
-is bracketed by barriers, and the reported time is the MAX over ranks
-(SURVEY.md §8e).  The HIP path itself needs a GPU; here the per-rank "step" is a
-CPU stand-in with a rank-dependent duration."""
+"""Multi-process path of bench.py on CPU (gloo, world_size 2), end to end through
+bench.main: each rank generates its own shard of images (weak: B images per rank;
+strong: the batch split over the ranks), the timed region is bracketed by barriers
+and the reported time is the MAX over ranks, and a sample of every rank's indices /
+outputs is all_gathered to rank 0 and checked against the oracle.
+The HIP op itself needs a GPU: here the per-rank step (bench.run_config) is a CPU
+stand-in that produces the op's outputs with the oracle and sleeps a rank-dependent
+time."""
+import json
 import os
 import socket
 import sys
@@ -17,6 +21,8 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+SMALL = dict(B=3, H=2)  # deit_base shape with 3 images of 2 heads per rank
+
 
 def _free_port():
     with socket.socket() as s:
@@ -24,41 +30,69 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import bench
-        c = dict(bench.CONFIGS["deit_base"], B=2, H=2)
-        q, k, v, bias = bench.make_inputs(c, rank)
-        # every rank's shard is its own images: gather a checksum of each
-        sums = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(sums, torch.tensor([q.sum(), k.sum(), v.sum()], dtype=torch.float64))
-        delay = 0.05 * (rank + 1)
-        elapsed = bench.timed_region(lambda: time.sleep(delay), world, lambda: None, torch.device("cpu"))
-        out[rank] = (elapsed, [s.tolist() for s in sums])
-    finally:
-        dist.destroy_process_group()
+def _stub_run(c, images, steps, warmup, device, world, traffic_json):
+    """CPU stand-in for run_config: the op's outputs from the oracle, a timed region of
+    rank-dependent length."""
+    import bench
+    from oracle import mx_oracle as O
+    q, k, v, bias = bench.make_inputs(c, images)
+    r = O.attention(q, k, v, c["scale"], k_top=c["k"], pred_mode=c["mode"], bias=bias, flush=c["bias"])
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    elapsed = bench.timed_region(lambda: time.sleep(0.05 * (rank + 1)), world, lambda: None, device)
+    stages = {s: 0.0 for s in bench.STAGES}
+    roof = {"frac": 0.0, "qa_pass": {"frac": 0.0}}
+    return elapsed, stages, roof, {}, torch.from_numpy(r["out"]), torch.from_numpy(r["idx"])
 
 
-def test_bench_timed_region_max_over_ranks_and_sharded_inputs():
-    world = 2
+def _worker(rank, world, port, argv, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), MXA_BENCH_BACKEND="gloo")
+    import bench
+    bench.CONFIGS["deit_base"] = dict(bench.CONFIGS["deit_base"], **SMALL)
+    res = bench.main(argv, run=_stub_run)
+    if rank == 0:
+        out["res"] = json.dumps(res)
+    dist.destroy_process_group()
+
+
+def _run_world(argv, world=2):
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    e0, sums0 = out[0]
-    e1, sums1 = out[1]
-    # both ranks report the same MAX, at least the slowest rank's step
-    assert e0 == e1
-    assert e0 >= 0.1
-    # rank shards differ, and each rank reproduces its shard deterministically
-    assert sums0 == sums1
-    assert sums0[0] != sums0[1]
+    mp.spawn(_worker, args=(world, port, argv, out), nprocs=world, join=True)
+    return json.loads(out["res"])
+
+
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_bench_main_two_ranks_gathers_and_checks_every_shard(scaling):
+    res = _run_world(["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-secondary", "--scaling", scaling,
+                      "--parity-images", "2"])
+    assert res["n_gpus"] == 2 and res["scaling"] == scaling
+    assert res["config"]["parallelism"] == "dp2"
+    # the MAX over ranks: at least the slower rank's region (0.1 s)
+    assert res["ms_per_step"] * res["steps"] >= 100.0
+    par = res["parity"]
+    assert par["ranks_checked"] == 2
+    assert par["idx_bitmatch"] == 1.0 and par["out_normwise_rel_err_max"] == 0.0
+    if scaling == "weak":  # 3 images per rank: ranks hold images 0-2 and 3-5, two checked each
+        assert res["config"]["global_batch"] == 6 and res["config"]["batch_per_gpu"] == 3
+        assert par["images_checked"] == 4
+        assert res["value"] == pytest.approx(6 * 197 * 3 / (res["ms_per_step"] * 3 / 1e3))
+    else:  # the 3-image batch split 2 + 1: one image of each rank checked (equal all_gather shapes)
+        assert res["config"]["global_batch"] == 3 and res["config"]["batch_per_gpu"] == 2
+        assert par["images_checked"] == 2
+
+
+def test_bench_shards_and_per_image_inputs():
     import bench
-    c = dict(bench.CONFIGS["deit_base"], B=2, H=2)
-    q1, _, _, _ = bench.make_inputs(c, 1)
-    assert np.isclose(float(q1.astype(np.float64).sum()), sums0[1][0])
+    c = dict(bench.CONFIGS["deit_base"], **SMALL)
+    assert bench.shard(c, 1, 2, "weak") == [3, 4, 5]
+    assert bench.shard(c, 0, 2, "strong") == [0, 1] and bench.shard(c, 1, 2, "strong") == [2]
+    assert sum((bench.shard(dict(c, B=256), r, 8, "strong") for r in range(8)), []) == list(range(256))
+    # an image is the same whatever shard it is generated in
+    q_a = bench.make_inputs(c, [0, 1, 2])[0][2]
+    q_b = bench.make_inputs(c, [2])[0][0]
+    assert np.array_equal(q_a, q_b)
 
 
 def test_bench_single_rank_timed_region_has_no_collectives():
@@ -69,17 +103,19 @@ def test_bench_single_rank_timed_region_has_no_collectives():
     assert not dist.is_initialized()
 
 
-def test_bench_stage_bytes_by_path():
-    """Algorithmic bytes per kernel: the split path's two kernels move
-    the fused kernel's inputs plus the 4-byte kept indices written once and read once."""
+def test_bench_byte_and_op_accounting():
+    """Algorithmic bytes per kernel and the SURVEY §8d totals."""
     import bench
     c = bench.CONFIGS["deit_base"]
     split = bench.stage_bytes(c, "rows_split")
-    fused = bench.stage_bytes(c, "rows_fused")
+    dense = bench.stage_bytes(c, "rows_fused")
     h, N, k = c["B"] * c["H"], c["N"], c["k"]
-    assert list(split)[:3] == list(fused)[:3] == ["rows_prep_q", "rows_prep_k", "cols_prep_v"]
-    assert split["select"] + split["finish"] == fused["fused"] + h * 8 * N * k
+    assert list(split) == list(dense) == list(bench.STAGES)
+    assert dense["select"] == 0 and split["finish"] - dense["finish"] == h * 4 * N * k
     assert bench.fused_min_bytes(c) == 716537856  # SURVEY.md §8d: 716.5 MB at DeiT-base b256
+    assert abs(bench.bytes_qa(c) - 633.2e6) < 0.1e6  # SURVEY.md §8d Bytes_qa
+    assert abs(bench.ops_gemm(c) - 30.52e9) < 0.01e9  # SURVEY.md §8d Ops_gemm
+    assert abs(bench.bytes_qa(bench.CONFIGS["dit_xl2"]) - 446.8e6) < 0.1e6
 
 
 def test_hbm_traffic_kernel_names_map_to_bench_stages():
@@ -87,8 +123,8 @@ def test_hbm_traffic_kernel_names_map_to_bench_stages():
     spec = importlib.util.spec_from_file_location("hbm_traffic", os.path.join(ROOT, "tools", "hbm_traffic.py"))
     ht = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ht)
-    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, false, 1>(mxa::Rows2Args)") == "select"
-    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, true, 2>(mxa::Rows2Args)") == "finish"
-    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 0, false, false, 0>(mxa::Rows2Args)") == "fused"
+    assert ht.stage_of("void mxa::select_kernel<256, 3>(mxa::Rows2Args)") == "select"
+    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, false, 2>(mxa::Rows2Args)") == "finish"
+    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 0, false, false, 0>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("mxa::rows_prep_kernel(mxa::RowsPrepArgs)") == "rows_prep"
     assert ht.stage_of("mxa::cols_prep_kernel(mxa::ColsPrepArgs)") == "cols_prep_v"

@@ -15,17 +15,14 @@ import sys
 
 
 def stage_of(kernel):
-    if "attn_rows2_kernel" in kernel:  # template <S, MODE, TOPK, BIG, PART>
-        part = kernel.split(">")[0].split(",")[-1].strip()
-        return {"1": "select", "2": "finish"}.get(part, "fused")
-    if "attn_rows_kernel" in kernel or "scores_topk_kernel" in kernel:
-        return "scores_topk"
+    if "select_kernel" in kernel:
+        return "select"
+    if "attn_rows2_kernel" in kernel:  # template <S, MODE, TOPK, BIG, PART>: 2 finishing, 0 dense
+        return "finish"
     if "rows_prep_kernel" in kernel:
         return "rows_prep"
     if "cols_prep_kernel" in kernel:
         return "cols_prep_v"
-    if "pv_kernel" in kernel:
-        return "pv"
     return None
 
 
