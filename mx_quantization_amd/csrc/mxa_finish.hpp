@@ -61,13 +61,14 @@ __device__ __forceinline__ float scale_f(int e) {
   return e == kExpNaN ? __uint_as_float(0x7FC00000u) : (e < -149 ? 0.0f : pow2f(e));
 }
 
-// KS: kept slots per lane (k <= 16 KS)
-template <int KS>
+// NB: 32-blocks per head dim (nbd); KS: kept slots per lane (k <= 16 KS)
+template <int NB, int KS>
 __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
   const int bh = blockIdx.x;
-  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
+  const int T = a.T, D = a.D, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
+  constexpr int nbd = NB;
   const int b_ = bh / a.H, h_ = bh % a.H;
   const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
@@ -104,26 +105,46 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   __syncthreads();
 
   const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
+  // a pass's global inputs (the row's query codes / exponents and kept indices),
+  // loaded one pass ahead so that their latency hides behind the previous pass
+  struct PassIn {
+    uint4 qv[2 * NB];
+    int qe[NB];
+    int ix[KS];
+  };
+  auto load_pass = [&](int r0, int pass, PassIn& in) {
+    const int r = r0 + 4 * pass + gi;
+    const bool valid = r < r_end;
+    const int64_t grow = (int64_t)bh * a.N + (valid ? r : r_beg);
+    const int8_t* qsrc = a.qc + grow * a.dpad;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      in.qv[2 * b] = *reinterpret_cast<const uint4*>(qsrc + 32 * b);
+      in.qv[2 * b + 1] = *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16);
+      in.qe[b] = exp_from16(a.qsT[grow * nbd + b]);
+    }
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const int s = gl + 16 * t;
+      in.ix[t] = valid && s < k ? a.idx32[grow * k + s] : -1;
+    }
+  };
+  PassIn nxt;
+  if (r_beg + kFinTile * wave < r_end) load_pass(r_beg + kFinTile * wave, 0, nxt);
   for (int r0 = r_beg + kFinTile * wave; r0 < r_end; r0 += kFinTile * a.waves) {
     // ---- 1. kept scores, softmax, MX(P) into the code tile: four rows per pass ----
     for (int pass = 0; pass < kFinTile / 4; ++pass) {
+      const PassIn cur = nxt;
+      if (pass + 1 < kFinTile / 4) load_pass(r0, pass + 1, nxt);
+      else if (r0 + kFinTile * a.waves < r_end) load_pass(r0 + kFinTile * a.waves, 0, nxt);
       const int tr = 4 * pass + gi;  // row within the tile
       const int r = r0 + tr;
       const bool valid = r < r_end;
       const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
       const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
-      const int8_t* qsrc = a.qc + grow * a.dpad;
-      uint4 qv[2 * kMaxNB];
-      int qe[kMaxNB];
-#pragma unroll
-      for (int b = 0; b < kMaxNB; ++b) {
-        qv[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b) : make_uint4(0, 0, 0, 0);
-        qv[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
-        qe[b] = b < nbd ? exp_from16(a.qsT[grow * nbd + b]) : 0;
-      }
       auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
         bool nan = false;
-        const double acc = g_dot<0>(qv, qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
+        const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
         float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
         if (brow) t = t + brow[(int64_t)j * a.bs3];
         return t;
@@ -136,10 +157,8 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        const int s = gl + 16 * t;
-        const bool kept = valid && s < k;
-        ix[t] = kept ? a.idx32[grow * k + s] : -1;
-        v[t] = kept ? true_of(ix[t]) : -INFINITY;
+        ix[t] = cur.ix[t];
+        v[t] = ix[t] >= 0 ? true_of(ix[t]) : -INFINITY;
         mx = fmaxf(mx, v[t]);
       }
       mx = __uint_as_float(row16_reduce(__float_as_uint(mx), [](uint32_t x, uint32_t y) {
@@ -154,7 +173,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
       sum = __uint_as_float(row16_reduce(__float_as_uint(sum), [](uint32_t x, uint32_t y) {
         return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
       }));
-      // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
+    // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
         if (ix[t] >= 0) {

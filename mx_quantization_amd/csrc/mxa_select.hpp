@@ -24,12 +24,12 @@ constexpr int kSelRows = 32;  // query rows per workgroup (a multiple of 4 * kSe
 // MX dot product of a query row (codes in registers, two uint4 per 32-block, block
 // exponents qe) with key row krow of the LDS code table: exact block sums by v_dot4,
 // block scale 2^(qe+ke) (MUL = 0) or qe*ke/4096 (EXION, MUL = 1), fp64 accumulation
-template <int MUL>
+template <int MUL, int NBMAX = kMaxNB>
 __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd, const int8_t* krow,
                                         const int16_t* kexp, bool& nan) {
   double acc = 0.0;
 #pragma unroll
-  for (int b = 0; b < kMaxNB; ++b) {
+  for (int b = 0; b < NBMAX; ++b) {
     if (b < nbd) {
       const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
       const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
