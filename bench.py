@@ -271,7 +271,7 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
         "bound": "hbm", "kernel": dom, "path": path,
         "limiter": ("instruction issue (VALU + LDS) of the exact-order top-k: the selection kernel moves "
                     "~2% of its duration's HBM bytes (PMC: profiles/r02_*)") if dom == "select" else
-                   ("VALU: v_dot4 gather of the kept keys' true scores and P.V, fp64 block epilogues"
+                   ("VALU: v_dot4 gather of the kept keys' true scores (fp64 block epilogue), softmax, MX(P)"
                     if dom == "finish" else None),
         "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
         "algorithmic_bytes_per_launch": by[dom], "mean_ms": stages[dom],
@@ -279,10 +279,12 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
                     "bytes": bytes_qa(cb), "ms": qa_ms, "achieved": qa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": qa_gbs / HBM_PEAK_GBS},
         "mfma": {"what": "SURVEY §8d Ops_gemm (dense QK^T + PV int8 ops) over the finishing kernel's time; "
-                         "that kernel computes the kept keys' QK^T and P.V with v_dot4 on LDS-resident "
-                         "MX blocks (no MFMA instructions), so this is an equivalent-rate fraction",
+                         "that kernel runs P.V on v_mfma_i32_32x32x32_i8 (one per 32-key MX block and 32 "
+                         "output columns of a 32-row P tile) and the kept keys' QK^T with v_dot4, so this "
+                         "is the dense-equivalent rate",
                  "ops": ops_gemm(cb), "ms": stages["finish"], "achieved": mf_tops, "peak": I8_PEAK_TOPS,
-                 "unit": "TOPS", "frac": mf_tops / I8_PEAK_TOPS, "engine": "v_dot4"},
+                 "unit": "TOPS", "frac": mf_tops / I8_PEAK_TOPS,
+                 "engine": "P.V: v_mfma_i32_32x32x32_i8; kept-key QK^T: v_dot4"},
     }
     e2e = {"fused_min_bytes": fused_min_bytes(cb),
            "achieved_GBs": fused_min_bytes(cb) / (sum(stages.values()) * 1e-3) / 1e9}
