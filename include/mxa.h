@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MXA_ABI_VERSION 1
+#define MXA_ABI_VERSION 2
 
 /* status codes */
 #define MXA_OK 0
@@ -52,6 +52,10 @@ extern "C" {
 #define MXA_PRED_PARTIAL_K 2
 #define MXA_PRED_MXINT4 3
 #define MXA_PRED_EXION 4
+#define MXA_PRED_TRUE_EX 5  /* exponent_based_sign_leading_ones (PixArt MX_transformer_block.py:663-664)   */
+#define MXA_PRED_ELSA 6     /* elsa_approximation.approximation_scores (funcs/elsa_approximation.py:115-143);
+                               self-attention only (N == T): the reference scales row n by the norm of
+                               key row n (:126, :142-143), which broadcasts only when N == T         */
 
 int mxa_abi_version(void);
 const char* mxa_status_string(int status);
@@ -105,9 +109,12 @@ int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64
  * as called at workloads/deit/scripts/main.py:123, workloads/DiT/models.py:194,
  * workloads/PixArt/models/MX_transformer_block.py:678, :825.
  * rows x n float32 with leading dim ld; n <= 512.  out_vals nullable.
+ * out_mask (nullable): the prune mask zeros.scatter_(-1, idx, 1) of the callers
+ * (deit main.py:147-148; examples/deit/top_k.py:16-42) as rows x ceil(n/32)
+ * words, bit j%32 of word j/32 set iff j is kept.
  */
 int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
-             int64_t* out_idx, float* out_vals, hipStream_t stream);
+             int64_t* out_idx, float* out_vals, uint32_t* out_mask, hipStream_t stream);
 
 /*
  * The fused hot path: MXINT8 true scores, approximate scores, top-k prune,
@@ -140,7 +147,14 @@ typedef struct mxa_attn_params {
   int64_t out_strides[3];
   int64_t* idx_out;        /* (B,H,N,k_top) contiguous int64, nullable                     */
   float* true_out;         /* optional (B,H,N,T) contiguous true scores (tests)            */
-  float* pred_out;         /* optional (B,H,N,T) contiguous approximate scores (tests)    */
+  float* pred_out;         /* optional (B,H,N,T) contiguous approximate scores            */
+  uint32_t* mask_out;      /* optional prune mask (B,H,N,ceil(T/32)) words: bit t%32 of word
+                              t/32 set iff key t is kept (zeros.scatter_(-1, idx, 1))      */
+  const float* elsa_proj;  /* MXA_PRED_ELSA: (D,D) row-major orthogonal matrix P of the
+                              caller; hash bit j = (MX(x) . P[j] >= 0)  (:105-112)           */
+  const float* elsa_cos;   /* MXA_PRED_ELSA: (D+1) floats cos(clamp(pi/D*h - 0.127, 0)), the
+                              caller's torch.cos values (:138-143); nullable: computed on the
+                              device, correctly rounded                                    */
   void* workspace;         /* device scratch of mxa_attention_workspace_bytes() bytes     */
   int64_t workspace_bytes;
 } mxa_attn_params;
@@ -149,15 +163,21 @@ int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p);
 int mxa_attention(const mxa_attn_params* p, hipStream_t stream);
 
 /*
+ * The approximate scores alone: pred = aQ @ aK^T (+ bias) for p->pred_mode into
+ * p->pred_out (required, (B,H,N,T) contiguous) -- what the callers compute from
+ * exponent_approximation's operands (deit main.py:101-118, DiT models.py:176-190,
+ * PixArt MX_transformer_block.py:658-677, :805-822) or ELSA's approximation_scores,
+ * without the top-k, softmax or P.V.  v and out are ignored (may be null).
+ */
+int mxa_approx_scores(const mxa_attn_params* p, hipStream_t stream);
+
+/*
  * Which kernels mxa_attention(p) runs (no launch; the workspace may be null):
  *   MXA_PATH_ROWS_SPLIT  selection kernel (scores + top-k) then finishing kernel
- *                        (gather, softmax, P, P.V) -- the default for top-k
- *   MXA_PATH_ROWS_FUSED  one row kernel for all of it (dense softmax, or MXA_ATTN_PATH=fused)
- *   MXA_PATH_ROWS_V1 / MXA_PATH_TILES  earlier layouts, kept for large heads
+ *                        (gather, softmax, MX(P), P.V on int8 MFMA) -- top_k != 0
+ *   MXA_PATH_ROWS_FUSED  one row kernel for all of it -- the dense branch (top_k == 0)
  * or a negative MXA_ERR_* for invalid parameters.
  */
-#define MXA_PATH_TILES 0
-#define MXA_PATH_ROWS_V1 1
 #define MXA_PATH_ROWS_FUSED 2
 #define MXA_PATH_ROWS_SPLIT 3
 int mxa_attention_path(const mxa_attn_params* p);

@@ -6,7 +6,8 @@ PyTorch-ROCm, exposed through
 
   * `mx_topk_attention` -- the fused path (MXINT8 QK^T, approximate scores,
     exact-order top-k, softmax, MXINT8 P.V),
-  * `topk` -- torch.topk with torch's CPU index order, on the device,
+  * `mx_approx_scores` -- the approximator's scores alone (pred = aQ @ aK^T, ELSA),
+  * `topk` -- torch.topk with torch's CPU index order (and the prune mask), on the device,
   * the reference's own operator surface, as drop-in packages:
       mx_quantization_amd.mx     (microxscaling `mx`: matmul, quantize_mx_op, ...)
       mx_quantization_amd.funcs  (`funcs`: exponent_approximation, ...)
@@ -16,15 +17,18 @@ PyTorch-ROCm, exposed through
 from ._native import NativeError, lib  # noqa: F401
 from .ops import (  # noqa: F401
     approx_values,
+    elsa_cos_table,
+    mx_approx_scores,
     mx_matmul,
     mx_topk_attention,
     quantize_bfloat,
     quantize_mx,
     shared_exponents,
     topk,
+    unpack_mask,
 )
 
-__all__ = ["mx_topk_attention", "topk", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
+__all__ = ["mx_topk_attention", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
 
 
 def install_dropin():

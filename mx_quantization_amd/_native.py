@@ -21,8 +21,10 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
-PATH_NAMES = {0: "tiles", 1: "rows_v1", 2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
-PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4}
+ABI_VERSION = 2
+PATH_NAMES = {2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
+PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4,
+              "true_ex": 5, "ELSA": 6}
 ROUND_MODES = {"nearest": 0, "floor": 1, "even": 2}
 
 
@@ -36,7 +38,8 @@ class AttnParams(ctypes.Structure):
         ("flush_subnormals", c_i32), ("bfloat", c_i32),
         ("bias", c_vp), ("bias_strides", c_i64 * 4),
         ("out", c_vp), ("out_strides", c_i64 * 3),
-        ("idx_out", c_vp), ("true_out", c_vp), ("pred_out", c_vp),
+        ("idx_out", c_vp), ("true_out", c_vp), ("pred_out", c_vp), ("mask_out", c_vp),
+        ("elsa_proj", c_vp), ("elsa_cos", c_vp),
         ("workspace", c_vp), ("workspace_bytes", c_i64),
     ]
 
@@ -49,9 +52,10 @@ _SIGS = {
     "mxa_shared_exponents": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     "mxa_quantize_bfloat": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
     "mxa_approx_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
-    "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mxa_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams)]),
     "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
+    "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_attention_path": (c_i32, [ctypes.POINTER(AttnParams)]),
     "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
@@ -83,7 +87,7 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.mxa_abi_version() != 1:
+        if handle.mxa_abi_version() != ABI_VERSION:
             raise NativeError("libmxa.so ABI version mismatch")
         _lib = handle
     return _lib

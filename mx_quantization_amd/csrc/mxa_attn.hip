@@ -27,7 +27,9 @@ enum RowsMode : int {
   kModeTrue = 0,   // row values are the true scores (approx off, or dense)
   kModeOpExp = 1,  // approximator codes, block scale 2^(sa + sb)
   kModeOpMul = 2,  // approximator codes, block scale sa * sb / 4096 (EXION)
-  kModeExSign = 3  // ex_pred: sign words + block exponents
+  kModeExSign = 3,  // ex_pred: sign words + block exponents
+  kModeTrueEx = 4,  // true_ex: power-of-two codes + zero indicators + block exponents
+  kModeElsa = 5     // ELSA: hash words, key norms, cosine table
 };
 
 // scalar (uniform-address) loads of a wave's query row
@@ -102,19 +104,32 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 // workspace regions, 256-B aligned
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qsT, qsA, qsg, kc, kop, ksT, ksA, ksg, vt, vs, idx32, total;
+  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx32, total;
 };
 
-AttnLayout attn_layout(const mxa_attn_params* p) {
+// the selection kernel's score mode of a call (ranked: the selection kernel runs)
+int score_mode(const mxa_attn_params* p, bool ranked) {
+  if (!(p->approx && ranked)) return kModeTrue;
+  switch (p->pred_mode) {
+    case MXA_PRED_EX_PRED: return kModeExSign;
+    case MXA_PRED_EXION: return kModeOpMul;
+    case MXA_PRED_TRUE_EX: return kModeTrueEx;
+    case MXA_PRED_ELSA: return kModeElsa;
+    default: return kModeOpExp;
+  }
+}
+
+AttnLayout attn_layout(const mxa_attn_params* p, int mode) {
   AttnLayout L{};
   const int64_t BH = (int64_t)p->B * p->H;
   L.nbd = (p->D + 31) / 32;
   L.dpad = L.nbd * 32;
   L.ntb = (p->T + 31) / 32;
   L.tpad = L.ntb * 32;
-  const bool need_pred = p->top_k && p->approx;
-  const bool op = need_pred && p->pred_mode != MXA_PRED_EX_PRED;  // approximator codes
-  const bool sg = need_pred && p->pred_mode == MXA_PRED_EX_PRED;  // ex_pred sign words
+  const bool need_pred = mode != kModeTrue;
+  const bool op = mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx;  // approximator codes
+  const bool sg = mode == kModeExSign || mode == kModeElsa;                         // sign / hash words
+  const bool sa = need_pred && mode != kModeElsa;                                   // approximator scales
   int64_t off = 0;
   auto take = [&](int64_t bytes) {
     const int64_t o = off;
@@ -124,14 +139,17 @@ AttnLayout attn_layout(const mxa_attn_params* p) {
   const int64_t qrows = BH * p->N, krows = BH * p->T;
   L.qc = take(qrows * L.dpad);
   L.qop = take(op ? qrows * L.dpad : 0);
+  L.qz = take(mode == kModeTrueEx ? qrows * L.dpad : 0);
   L.qsT = take(qrows * L.nbd * 2);
-  L.qsA = take(need_pred ? qrows * L.nbd * 2 : 0);
+  L.qsA = take(sa ? qrows * L.nbd * 2 : 0);
   L.qsg = take(sg ? qrows * L.nbd * 4 : 0);
   L.kc = take(krows * L.dpad);
   L.kop = take(op ? krows * L.dpad : 0);
+  L.kz = take(mode == kModeTrueEx ? krows * L.dpad : 0);
   L.ksT = take(krows * L.nbd * 2);
-  L.ksA = take(need_pred ? krows * L.nbd * 2 : 0);
+  L.ksA = take(sa ? krows * L.nbd * 2 : 0);
   L.ksg = take(sg ? krows * L.nbd * 4 : 0);
+  L.knorm = take(mode == kModeElsa ? krows * 4 : 0);
   L.vt = take(BH * p->D * (int64_t)L.tpad);
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
   L.idx32 = take(p->top_k ? qrows * (int64_t)p->k_top * 4 : 0);
@@ -158,50 +176,49 @@ extern "C" const char* mxa_status_string(int status) {
 
 extern "C" int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p) {
   if (!p || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return -1;
-  return attn_layout(p).total;
+  // sized for the approximator whenever it may run (top-k, or the scores alone)
+  return attn_layout(p, score_mode(p, p->top_k || p->pred_out)).total;
 }
 
-// ---- finishing (part 2) and dense (part 0) row kernels (mxa_rows2.hpp) ----------
-static size_t rows2_total(int mode, const Rows2Args& ra, int S, int W, int part) {
-  return rows2_lds(mode, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, S, ra.tpad, ra.k_top, W, part).total;
+// ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
+static size_t rows2_total(const Rows2Args& ra, int W) {
+  return rows2_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.tpad, W).total;
 }
 // waves per workgroup: the size (8 or 16) that keeps the most waves resident per CU
-// (LDS-limited workgroups x waves, capped by the kernel's 7-waves-per-SIMD register
-// use): DeiT-base 8, DiT 16 (larger K / V tables: 2 workgroups per CU either way)
-static int rows2_waves(int mode, const Rows2Args& ra, int S, int part) {
+// (LDS-limited workgroups x waves, capped by the kernel's 7-waves-per-SIMD register use)
+static int rows2_waves(const Rows2Args& ra) {
   auto resident = [&](int w) {
-    const size_t t = rows2_total(mode, ra, S, w, part);
+    const size_t t = rows2_total(ra, w);
     return t > 160 * 1024 ? 0 : std::min((int)(160 * 1024 / t) * w, 28);
   };
   const int r8 = resident(8), r16 = resident(16);
   if (r8 > 0 || r16 > 0) return r16 > r8 ? 16 : 8;
-  return rows2_total(mode, ra, S, 4, part) <= 160 * 1024 ? 4 : 0;
+  return rows2_total(ra, 4) <= 160 * 1024 ? 4 : 0;
 }
 
-template <int S, int MODE, bool TOPK, int PART>
-static int launch_rows2_p(const Rows2Args& ra0, int BH, hipStream_t stream) {
+template <int S>
+static int launch_dense_s(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
   Rows2Args ra = ra0;
-  ra.waves = rows2_waves(MODE, ra, S, PART);
+  ra.waves = rows2_waves(ra);
   if (ra.waves <= 0) return MXA_ERR_UNSUPPORTED;
-  const size_t lds = rows2_total(MODE, ra, S, ra.waves, PART);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_rows2_kernel<S, MODE, TOPK, false, PART>),
+  if (plan) return MXA_OK;
+  const size_t lds = rows2_total(ra, ra.waves);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&dense_rows_kernel<S>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
-  // few heads (PixArt cross-attention: 128): split each head's rows over grid.y so
-  // that the launch still has ~4 workgroups per CU
+  // few heads: split each head's rows over grid.y so that the launch still has ~4
+  // workgroups per CU
   const int chunks = std::max(1, std::min((ra.N + ra.waves - 1) / ra.waves, 1024 / std::max(BH, 1)));
   ra.rows_per_wg = (ra.N + chunks - 1) / chunks;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((attn_rows2_kernel<S, MODE, TOPK, false, PART>), dim3((unsigned)BH, gy), dim3(64 * ra.waves),
-                     lds, stream, ra);
+  hipLaunchKernelGGL(dense_rows_kernel<S>, dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
 // ---- selection kernel (mxa_select.hpp): four query rows per wave -------------------
 template <int NP, int MODE>
 static size_t select_lds(const Rows2Args& ra) {
-  return rows2_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, 1, ra.tpad, 0, 0, 1).waves +
-         (size_t)4 * kSelWaves * grp_row_bytes(grp_alloc(ra.T), NP);
+  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * kSelWaves * grp_row_bytes(grp_alloc(ra.T), NP);
 }
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
@@ -231,6 +248,8 @@ static int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stre
     case kModeOpExp: return launch_select_m<kModeOpExp>(ra, BH, stream, plan);
     case kModeOpMul: return launch_select_m<kModeOpMul>(ra, BH, stream, plan);
     case kModeExSign: return launch_select_m<kModeExSign>(ra, BH, stream, plan);
+    case kModeTrueEx: return launch_select_m<kModeTrueEx>(ra, BH, stream, plan);
+    case kModeElsa: return launch_select_m<kModeElsa>(ra, BH, stream, plan);
     default: return launch_select_m<kModeTrue>(ra, BH, stream, plan);
   }
 }
@@ -301,11 +320,6 @@ static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool p
 }
 
 // the row kernel of the path: the finishing kernel (top-k) or the dense kernel
-template <int S>
-static int launch_rows_s(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (plan) return rows2_waves(kModeTrue, ra, S, 0) > 0 ? MXA_OK : MXA_ERR_UNSUPPORTED;  // feasibility only
-  return launch_rows2_p<S, kModeTrue, false, 0>(ra, BH, stream);
-}
 static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan) {
   if (topk) {
     // the selection kernel already wrote the true scores when it ranked them
@@ -314,124 +328,163 @@ static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, in
     return launch_finish(rf, BH, stream, plan);
   }
   switch (S) {
-    case 1: return launch_rows_s<1>(ra, BH, stream, plan);
-    case 2: return launch_rows_s<2>(ra, BH, stream, plan);
-    case 4: return launch_rows_s<4>(ra, BH, stream, plan);
-    default: return launch_rows_s<8>(ra, BH, stream, plan);
+    case 1: return launch_dense_s<1>(ra, BH, stream, plan);
+    case 2: return launch_dense_s<2>(ra, BH, stream, plan);
+    case 4: return launch_dense_s<4>(ra, BH, stream, plan);
+    default: return launch_dense_s<8>(ra, BH, stream, plan);
   }
 }
 
-// plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing
-static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr) {
-  if (!p || !p->q || !p->k || !p->v || !p->out) return MXA_ERR_ARG;
+// plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing;
+// scores_only: the approximate (or true) scores into p->pred_out / true_out, no top-k
+static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr,
+                          bool scores_only = false) {
+  if (!p || !p->q || !p->k) return MXA_ERR_ARG;
+  if (!scores_only && (!p->v || !p->out)) return MXA_ERR_ARG;
+  if (scores_only && !(p->approx ? p->pred_out : p->true_out)) return MXA_ERR_ARG;
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
-  if (p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
-  if (p->pred_mode < MXA_PRED_EX_PRED || p->pred_mode > MXA_PRED_EXION) return MXA_ERR_ARG;
+  if (!scores_only && p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
+  if (p->pred_mode < MXA_PRED_EX_PRED || p->pred_mode > MXA_PRED_ELSA) return MXA_ERR_ARG;
   if (p->bfloat != 0 && p->bfloat != 32 && (p->bfloat < 10 || p->bfloat > 31)) return MXA_ERR_ARG;
   if (p->T > 512 || p->D > 32 * kMaxNB) return MXA_ERR_UNSUPPORTED;
-  const AttnLayout L = attn_layout(p);
-  const int64_t BH = (int64_t)p->B * p->H;
+  mxa_attn_params pp = *p;
+  if (scores_only) {  // the selection kernel alone, with no kept keys
+    pp.top_k = 0;
+    pp.k_top = 0;
+    pp.idx_out = nullptr;
+    pp.mask_out = nullptr;
+  }
+  const bool topk = pp.top_k != 0;
+  const bool ranked = topk || scores_only;  // the selection kernel runs
+  const int mode = score_mode(&pp, ranked);
+  if (mode == kModeElsa && (!pp.elsa_proj || pp.N != pp.T)) return MXA_ERR_ARG;  // elsa_approximation.py:126, :142
+  const AttnLayout L = attn_layout(&pp, mode);
+  const int64_t BH = (int64_t)pp.B * pp.H;
 
   int opq = MXA_OP_SIGN, opk = MXA_OP_SIGN;
-  switch (p->pred_mode) {
+  switch (pp.pred_mode) {
     case MXA_PRED_PARTIAL_Q: opq = MXA_OP_MXINT8; break;  // Q = MXINT8, K = exp-sign
     case MXA_PRED_PARTIAL_K: opk = MXA_OP_MXINT8; break;  // Q = exp-sign, K = MXINT8
     case MXA_PRED_MXINT4: opq = opk = MXA_OP_MXINT4; break;
     case MXA_PRED_EXION: opq = opk = MXA_OP_EXION; break;
+    case MXA_PRED_TRUE_EX: opq = opk = MXA_OP_TRUE_EX; break;
     default: break;
   }
-  const bool topk = p->top_k != 0;
-  const bool need_pred = topk && p->approx;
-  const int S0 = (p->T + 63) / 64;
+  const int S0 = (pp.T + 63) / 64;
   const int S = S0 <= 1 ? 1 : (S0 <= 2 ? 2 : (S0 <= 4 ? 4 : 8));
-  const int mode = !need_pred ? kModeTrue
-                   : p->pred_mode == MXA_PRED_EX_PRED ? kModeExSign
-                   : p->pred_mode == MXA_PRED_EXION   ? kModeOpMul
-                                                      : kModeOpExp;
   Rows2Args r2{};
-  r2.B = p->B; r2.H = p->H; r2.N = p->N; r2.T = p->T; r2.D = p->D;
-  r2.nbd = L.nbd; r2.dpad = L.dpad; r2.ntb = L.ntb; r2.tpad = L.tpad; r2.k_top = topk ? p->k_top : 0;
+  r2.B = pp.B; r2.H = pp.H; r2.N = pp.N; r2.T = pp.T; r2.D = pp.D;
+  r2.nbd = L.nbd; r2.dpad = L.dpad; r2.ntb = L.ntb; r2.tpad = L.tpad; r2.k_top = topk ? pp.k_top : 0;
   r2.kst = L.dpad + 16;  // conflict-free b128 reads of the LDS code tables
   r2.vst = L.tpad + 16;
   // feasibility of the path's kernels (LDS budgets)
-  int rc = launch_rows(r2, topk, mode == kModeTrue, S, (int)BH, stream, true);
-  if (!rc && topk) rc = launch_select(r2, mode, (int)BH, stream, true);
+  int rc = scores_only ? MXA_OK : launch_rows(r2, topk, mode == kModeTrue, S, (int)BH, stream, true);
+  if (!rc && ranked) rc = launch_select(r2, mode, (int)BH, stream, true);
   if (rc) return rc;
   if (plan) {
     *plan = topk ? MXA_PATH_ROWS_SPLIT : MXA_PATH_ROWS_FUSED;
     return MXA_OK;
   }
-  if (!p->workspace || p->workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
-  unsigned char* ws = static_cast<unsigned char*>(p->workspace);
+  if (!pp.workspace || pp.workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
+  unsigned char* ws = static_cast<unsigned char*>(pp.workspace);
   if (!aligned16(ws)) return MXA_ERR_ARG;
-  const bool need_op = need_pred && mode != kModeExSign;
+  const bool need_op = mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx;
+  const bool need_sa = mode != kModeTrue && mode != kModeElsa;
 
   RowsPrepArgs rq{};
-  rq.x = p->q; rq.s0 = p->q_strides[0]; rq.s1 = p->q_strides[1]; rq.s2 = p->q_strides[2];
-  rq.H = p->H; rq.R = p->N; rq.rows = BH * p->N; rq.D = p->D; rq.nb = L.nbd; rq.dpad = L.dpad;
-  rq.vec4 = aligned16(p->q) && (p->q_strides[0] % 4 == 0) && (p->q_strides[1] % 4 == 0) && (p->q_strides[2] % 4 == 0);
-  rq.op_kind = opq; rq.flush = p->flush_subnormals; rq.bfloat = p->bfloat;
+  rq.x = pp.q; rq.s0 = pp.q_strides[0]; rq.s1 = pp.q_strides[1]; rq.s2 = pp.q_strides[2];
+  rq.H = pp.H; rq.R = pp.N; rq.rows = BH * pp.N; rq.D = pp.D; rq.nb = L.nbd; rq.dpad = L.dpad;
+  rq.vec4 = aligned16(pp.q) && (pp.q_strides[0] % 4 == 0) && (pp.q_strides[1] % 4 == 0) && (pp.q_strides[2] % 4 == 0);
+  rq.op_kind = opq; rq.flush = pp.flush_subnormals; rq.bfloat = pp.bfloat;
   rq.codes = reinterpret_cast<int8_t*>(ws + L.qc);
   rq.sT = reinterpret_cast<int16_t*>(ws + L.qsT);
   rq.op = need_op ? reinterpret_cast<int8_t*>(ws + L.qop) : nullptr;
+  rq.zind = mode == kModeTrueEx ? reinterpret_cast<int8_t*>(ws + L.qz) : nullptr;
   rq.signs = mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.qsg) : nullptr;
-  rq.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
+  rq.sA = need_sa ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
   if (ev) (void)hipEventRecord(ev[0], stream);
   rc = launch_rows_prep(rq, stream);
   if (rc) return rc;
   if (ev) (void)hipEventRecord(ev[1], stream);
 
   RowsPrepArgs rk = rq;
-  rk.x = p->k; rk.s0 = p->k_strides[0]; rk.s1 = p->k_strides[1]; rk.s2 = p->k_strides[2];
-  rk.R = p->T; rk.rows = BH * p->T;
-  rk.vec4 = aligned16(p->k) && (p->k_strides[0] % 4 == 0) && (p->k_strides[1] % 4 == 0) && (p->k_strides[2] % 4 == 0);
+  rk.x = pp.k; rk.s0 = pp.k_strides[0]; rk.s1 = pp.k_strides[1]; rk.s2 = pp.k_strides[2];
+  rk.R = pp.T; rk.rows = BH * pp.T;
+  rk.vec4 = aligned16(pp.k) && (pp.k_strides[0] % 4 == 0) && (pp.k_strides[1] % 4 == 0) && (pp.k_strides[2] % 4 == 0);
   rk.op_kind = opk;
   rk.codes = reinterpret_cast<int8_t*>(ws + L.kc);
   rk.sT = reinterpret_cast<int16_t*>(ws + L.ksT);
   rk.op = need_op ? reinterpret_cast<int8_t*>(ws + L.kop) : nullptr;
+  rk.zind = mode == kModeTrueEx ? reinterpret_cast<int8_t*>(ws + L.kz) : nullptr;
   rk.signs = mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.ksg) : nullptr;
-  rk.sA = need_pred ? reinterpret_cast<int16_t*>(ws + L.ksA) : nullptr;
+  rk.sA = need_sa ? reinterpret_cast<int16_t*>(ws + L.ksA) : nullptr;
   rc = launch_rows_prep(rk, stream);
   if (rc) return rc;
+  if (mode == kModeElsa) {  // hashes of MX(Q), MX(K); norms of MX(K) rows
+    ElsaPrepArgs eq{};
+    eq.codes = rq.codes; eq.sT = rq.sT; eq.proj = pp.elsa_proj; eq.rows = rq.rows;
+    eq.D = pp.D; eq.nb = L.nbd; eq.dpad = L.dpad;
+    eq.hash = reinterpret_cast<uint32_t*>(ws + L.qsg);
+    rc = launch_elsa_prep(eq, stream);
+    if (rc) return rc;
+    ElsaPrepArgs ek = eq;
+    ek.codes = rk.codes; ek.sT = rk.sT; ek.rows = rk.rows;
+    ek.hash = reinterpret_cast<uint32_t*>(ws + L.ksg);
+    ek.norm = reinterpret_cast<float*>(ws + L.knorm);
+    rc = launch_elsa_prep(ek, stream);
+    if (rc) return rc;
+  }
   if (ev) (void)hipEventRecord(ev[2], stream);
 
-  ColsPrepArgs cv{};
-  cv.x = p->v; cv.s0 = p->v_strides[0]; cv.s1 = p->v_strides[1]; cv.s2 = p->v_strides[2];
-  cv.H = p->H; cv.mats = BH; cv.R = p->T; cv.C = p->D; cv.nb = L.ntb; cv.rpad = L.tpad;
-  cv.mbits = 8; cv.flush = p->flush_subnormals; cv.bfloat = p->bfloat;
-  cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
-  cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
-  rc = launch_cols_prep(cv, stream);
-  if (rc) return rc;
+  if (!scores_only) {
+    ColsPrepArgs cv{};
+    cv.x = pp.v; cv.s0 = pp.v_strides[0]; cv.s1 = pp.v_strides[1]; cv.s2 = pp.v_strides[2];
+    cv.H = pp.H; cv.mats = BH; cv.R = pp.T; cv.C = pp.D; cv.nb = L.ntb; cv.rpad = L.tpad;
+    cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat;
+    cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
+    cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
+    rc = launch_cols_prep(cv, stream);
+    if (rc) return rc;
+  }
   if (ev) (void)hipEventRecord(ev[3], stream);
 
   r2.qc = reinterpret_cast<const int8_t*>(ws + L.qc);
   r2.qop = reinterpret_cast<const int8_t*>(ws + L.qop);
+  r2.qz = reinterpret_cast<const int8_t*>(ws + L.qz);
   r2.qsT = reinterpret_cast<const int16_t*>(ws + L.qsT);
   r2.qsA = reinterpret_cast<const int16_t*>(ws + L.qsA);
   r2.qsg = reinterpret_cast<const uint32_t*>(ws + L.qsg);
   r2.kc = reinterpret_cast<const int8_t*>(ws + L.kc);
   r2.kop = reinterpret_cast<const int8_t*>(ws + L.kop);
+  r2.kz = reinterpret_cast<const int8_t*>(ws + L.kz);
   r2.ksT = reinterpret_cast<const int16_t*>(ws + L.ksT);
   r2.ksA = reinterpret_cast<const int16_t*>(ws + L.ksA);
   r2.ksg = reinterpret_cast<const uint32_t*>(ws + L.ksg);
+  r2.knorm = reinterpret_cast<const float*>(ws + L.knorm);
+  r2.elsa_cos = pp.elsa_cos;
   r2.vt = reinterpret_cast<const int8_t*>(ws + L.vt);
   r2.vs = reinterpret_cast<const int16_t*>(ws + L.vs);
-  r2.bfloat = p->bfloat; r2.flush_p = p->flush_subnormals; r2.scale = p->scale;
-  r2.bias = p->bias;
-  r2.bs0 = p->bias_strides[0]; r2.bs1 = p->bias_strides[1]; r2.bs2 = p->bias_strides[2]; r2.bs3 = p->bias_strides[3];
-  r2.out = p->out; r2.os0 = p->out_strides[0]; r2.os1 = p->out_strides[1]; r2.os2 = p->out_strides[2];
-  r2.idx_out = p->idx_out; r2.true_out = p->true_out; r2.pred_out = p->pred_out;
+  r2.bfloat = pp.bfloat; r2.flush_p = pp.flush_subnormals; r2.scale = pp.scale;
+  r2.bias = pp.bias;
+  r2.bs0 = pp.bias_strides[0]; r2.bs1 = pp.bias_strides[1]; r2.bs2 = pp.bias_strides[2]; r2.bs3 = pp.bias_strides[3];
+  r2.out = pp.out; r2.os0 = pp.out_strides[0]; r2.os1 = pp.out_strides[1]; r2.os2 = pp.out_strides[2];
+  r2.idx_out = pp.idx_out; r2.true_out = pp.true_out; r2.pred_out = pp.pred_out; r2.mask_out = pp.mask_out;
   r2.idx32 = reinterpret_cast<int32_t*>(ws + L.idx32);
-  if (topk) {
+  if (ranked) {
     rc = launch_select(r2, mode, (int)BH, stream, false);
     if (rc) return rc;
   }
   if (ev) (void)hipEventRecord(ev[4], stream);
-  rc = launch_rows(r2, topk, mode == kModeTrue, S, (int)BH, stream, false);
-  if (rc) return rc;
+  if (!scores_only) {
+    rc = launch_rows(r2, topk, mode == kModeTrue, S, (int)BH, stream, false);
+    if (rc) return rc;
+  }
   if (ev) (void)hipEventRecord(ev[5], stream);
   return MXA_OK;
+}
+
+extern "C" int mxa_approx_scores(const mxa_attn_params* p, hipStream_t stream) {
+  return attention_impl(p, stream, nullptr, nullptr, true);
 }
 
 extern "C" int mxa_attention(const mxa_attn_params* p, hipStream_t stream) {
@@ -479,11 +532,16 @@ static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t str
 }
 
 extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
-                        float* out_vals, hipStream_t stream) {
+                        float* out_vals, uint32_t* out_mask, hipStream_t stream) {
   if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
   if (n > 512) return MXA_ERR_UNSUPPORTED;
-  if (rows == 0 || k == 0) return MXA_OK;
-  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals};
+  if (rows == 0) return MXA_OK;
+  if (k == 0) {
+    if (out_mask) return hipMemsetAsync(out_mask, 0, (size_t)rows * ((n + 31) / 32) * 4, stream) == hipSuccess
+                             ? MXA_OK : MXA_ERR_LAUNCH;
+    return MXA_OK;
+  }
+  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask};
   const unsigned grid = (unsigned)((rows + 15) / 16);
   if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
   if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);

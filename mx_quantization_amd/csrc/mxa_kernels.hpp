@@ -44,6 +44,20 @@ struct RowsPrepArgs {
   int8_t* op;     // [rows][dpad] approximator operand (nullable)
   int16_t* sA;    // [rows][nb] approximator scale (nullable)
   uint32_t* signs;  // [rows][nb] bit i = (MX code i < 0) (nullable)
+  int8_t* zind;     // [rows][dpad] 1 where the MX code is 0 (column < D), else 0 (true_ex; nullable)
+};
+
+// ELSA sign hashes (and key norms) of rows already quantized by rows_prep:
+// hash bit j of a row = (sum_i MX_i * P[j][i] >= 0), norm = ||MX row||_2
+// (funcs/elsa_approximation.py:105-112, :126)
+struct ElsaPrepArgs {
+  const int8_t* codes;  // [rows][dpad]
+  const int16_t* sT;    // [rows][nb] exponent of a code unit
+  const float* proj;    // [D][D] row-major P
+  int64_t rows;
+  int D, nb, dpad;
+  uint32_t* hash;  // [rows][nb] hash words
+  float* norm;     // [rows] (nullable)
 };
 
 // matrices (R x C) at x + b*s0 + h*s1 + r*s2 + c quantized along R in 32-blocks
@@ -59,6 +73,7 @@ struct ColsPrepArgs {
 
 int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream);
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream);
+int launch_elsa_prep(const ElsaPrepArgs& a, hipStream_t stream);
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 

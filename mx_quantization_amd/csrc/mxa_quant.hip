@@ -11,6 +11,8 @@
 // reduced with lane shuffles, int8 codes + int16 block exponents written out.
 #include "mxa_kernels.hpp"
 
+#include <algorithm>
+
 namespace mxa {
 
 // ---------------------------------------------------------------------------
@@ -199,6 +201,20 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
       sA = eA;
       break;
     }
+    case MXA_OP_TRUE_EX:
+      // exponent_based_sign_leading_ones (examples/deit/exponent_based_prediction.py:163-178):
+      // (mx < 0 ? -1 : 1) * 2^floor(log2|mx|), zeros -> +1.  Nonzero elements as the
+      // power-of-two code sign * 2^floor(log2|code|) in units of 2^(es-6); zeros in zind
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ac = code[j] < 0 ? -code[j] : code[j];
+        const int p2 = ac ? 1 << (31 - __clz(ac)) : 0;
+        op[j] = code[j] < 0 ? -p2 : p2;
+      }
+      // a NaN block's MX values are NaN, and get_true_exponents maps them like zeros
+      // (mask |x| > 0 is false: exponent 0, value +1; examples :98-110): codes 0, zind 1
+      sA = nanblk ? 0 : es - 6;
+      break;
     default:  // MXA_OP_MXINT8
 #pragma unroll
       for (int j = 0; j < 4; ++j) op[j] = code[j];
@@ -213,6 +229,12 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
                         ((uint32_t)(op[2] & 0xFF) << 16) | ((uint32_t)(op[3] & 0xFF) << 24);
     if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
     if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
+    if (a.zind) {
+      uint32_t pz = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pz |= (c0 + j < a.D && code[j] == 0 ? 1u : 0u) << (8 * j);
+      *reinterpret_cast<uint32_t*>(a.zind + base) = pz;
+    }
   }
   // packed sign word of the block, bit (4*sub + j) = (code < 0): the exp-sign
   // operand of ex_pred (codes beyond D are 0, i.e. positive)
@@ -284,6 +306,51 @@ __global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// ELSA hashes / key norms (funcs/elsa_approximation.py:105-112, :126), one wave
+// per row: lane j (and j + 64) forms projected_j = sum_i MX_i * P[j][i] with P^T
+// staged in LDS (lane-contiguous reads), MX_i = code_i * 2^e exact in fp64, the
+// products exact in fp64 (8 x 24 bits); hash bit j = (projected_j >= 0) by ballot.
+// norm = sqrt(exact sum of MX_i^2) rounded once (torch.norm's result on these rows).
+// ---------------------------------------------------------------------------
+constexpr int kElsaWaves = 4;
+__global__ __launch_bounds__(64 * kElsaWaves) void elsa_prep_kernel(ElsaPrepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* pt = reinterpret_cast<float*>(smem);  // pt[i * D + j] = P[j][i]
+  const int D = a.D;
+  for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+    const int j = t / D, i = t - j * D;
+    pt[i * D + j] = a.proj[t];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * kElsaWaves + wave; row < a.rows; row += (int64_t)gridDim.x * kElsaWaves) {
+    const int8_t* cr = a.codes + row * a.dpad;
+    double acc0 = 0.0, acc1 = 0.0, nrm = 0.0;
+    bool nan = false;
+    for (int b = 0; b < a.nb; ++b) {
+      const int e = exp_from16(a.sT[row * a.nb + b]);
+      nan = nan || e == kExpNaN;
+      const double s = nan ? 0.0 : pow2d(e);
+      const int i1 = min(32, D - 32 * b);
+      for (int ii = 0; ii < i1; ++ii) {
+        const int i = 32 * b + ii;
+        const double x = (double)cr[i] * s;  // uniform
+        nrm += x * x;
+        acc0 += x * (double)pt[i * D + min(lane, D - 1)];
+        if (D > 64) acc1 += x * (double)pt[i * D + min(lane + 64, D - 1)];
+      }
+    }
+    const uint64_t h0 = __builtin_amdgcn_ballot_w64(!nan && lane < D && acc0 >= 0.0);
+    const uint64_t h1 = __builtin_amdgcn_ballot_w64(!nan && lane + 64 < D && acc1 >= 0.0);
+    if (lane < a.nb) {
+      const uint64_t h = lane < 2 ? h0 : h1;
+      a.hash[row * a.nb + lane] = (uint32_t)((lane & 1) ? h >> 32 : h);
+    }
+    if (a.norm && lane == 0) a.norm[row] = nan ? __uint_as_float(0x7FC00000u) : (float)sqrt(nrm);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // approximator operand VALUES (what exponent_approximation's methods return)
 // one thread per (row, 32-block); exact fp32 op order of the reference.
 // ---------------------------------------------------------------------------
@@ -319,7 +386,7 @@ __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
     if (flush) xv = xv * 0.0f;
     float out;
     if (nanblk) {
-      out = qnan;
+      out = a.op_kind == MXA_OP_TRUE_EX ? 1.0f : qnan;  // true_ex: NaN -> exponent 0 -> +1 (examples :98-110)
     } else if (a.op_kind == MXA_OP_MXINT4) {
       out = (round_code(xv, es, 4, kRoundNearest) * 0.25f) * pow2f(es);
     } else {
@@ -424,6 +491,17 @@ int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream) {
   if (threads == 0) return MXA_OK;
   if (a.rows * a.nb >= ((int64_t)1 << 28)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices (x8 lanes)
   hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+int launch_elsa_prep(const ElsaPrepArgs& a, hipStream_t stream) {
+  if (a.rows == 0) return MXA_OK;
+  if (a.D > 128 || a.nb > 4) return MXA_ERR_UNSUPPORTED;
+  const size_t lds = (size_t)a.D * a.D * 4;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&elsa_prep_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const int64_t blocks = std::min<int64_t>((a.rows + kElsaWaves - 1) / kElsaWaves, 2048);
+  hipLaunchKernelGGL(elsa_prep_kernel, dim3((unsigned)blocks), dim3(64 * kElsaWaves), lds, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream) {

@@ -1,14 +1,11 @@
-// Row kernels of the attention core, one wave per query row:
-//   PART 2, the finishing kernel of the top-k path: for the k kept indices of the row
-//      (select_kernel, mxa_select.hpp) lane l < k recomputes the true score of the l-th
-//      kept key (v_dot4 over the LDS codes, exact fp64 block epilogue),
-//      softmax over the kept scores (DPP reductions), P MX-quantized along keys (block
-//      maxima by LDS atomic max) into a dense LDS code row that is zero elsewhere, and
-//      out[d] = sum_b 2^(eP_b + eV_bd) * sum_{t in b} P_t V_td (v_dot4 of the P row
-//      against lane d's V^T row, fp64 block epilogue);
-//   PART 0, the dense branch (top_k=False): all T true scores, softmax, MX(P), P.V.
-// The head's K codes + exponents and V^T codes + exponents are staged in LDS once
-// per workgroup.
+// The dense branch (top_k=False: DeiT block 11, DiT / PixArt excluded timesteps,
+// SURVEY.md §8a a13), one wave per query row: all T true scores (v_dot4 over the LDS
+// codes, exact fp64 block epilogue), softmax over every key (DPP
+// reductions), P MX-quantized along keys into an LDS code row, and
+//   out[d] = sum_b 2^(eP_b + eV_bd) * sum_{t in b} P_t V_td
+// (v_dot4 of the P row against lane d's V^T row, fp64 block epilogue).  The head's K
+// codes + exponents and V^T codes + exponents are staged in LDS once per workgroup.
+// Also home of Rows2Args, the argument block of the selection / finishing kernels.
 // Callers: workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
 // workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859; the MX matmul
 // of P.V: microxscaling/mx/matmul.py:68-76.
@@ -19,13 +16,15 @@ namespace mxa {
 
 struct Rows2Args {
   // query side (rows_prep outputs)
-  const int8_t *qc, *qop;
+  const int8_t *qc, *qop, *qz;
   const int16_t *qsT, *qsA;
-  const uint32_t* qsg;
+  const uint32_t* qsg;  // ex_pred sign words / ELSA hash words
   // key side
-  const int8_t *kc, *kop;
+  const int8_t *kc, *kop, *kz;
   const int16_t *ksT, *ksA;
   const uint32_t* ksg;
+  const float* knorm;     // ELSA: key row norms
+  const float* elsa_cos;  // ELSA: (D+1) cosine table (nullable)
   // value side (cols_prep outputs: V^T codes [BH][D][tpad], exps [BH][ntb][D])
   const int8_t* vt;
   const int16_t* vs;
@@ -40,6 +39,7 @@ struct Rows2Args {
   int64_t* idx_out;
   float* true_out;
   float* pred_out;
+  uint32_t* mask_out;
   int waves;        // waves per workgroup
   int rows_per_wg;  // query rows per workgroup (grid.y splits a head when there are few heads)
   int32_t* idx32;  // split path: the kept indices [B*H*N][k_top] between the two kernels
@@ -47,37 +47,26 @@ struct Rows2Args {
 
 
 struct Rows2Lds {
-  size_t mx, sT, op, sA, sg, vt, vs, waves, per_wave, total;
+  size_t mx, sT, vt, vs, waves, per_wave, total;
 };
 
 __host__ __device__ inline size_t r2_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// part: 0 the fused kernel; 1 the selection kernel (scores + top-k, writes the
-// kept indices); 2 the finishing kernel (gather, softmax, P, P.V from the indices)
-__host__ __device__ inline Rows2Lds rows2_lds(int mode, int T, int D, int kst, int nbd, int vst, int ntb, int S,
-                                              int tpad, int k_top, int waves, int part = 0) {
+// LDS of the dense kernel: K codes + exponents, V^T codes + exponents, then per wave
+// the P code row, P block exponents and block maxima (16 each)
+__host__ __device__ inline Rows2Lds rows2_lds(int T, int D, int kst, int nbd, int vst, int ntb, int tpad, int waves) {
   Rows2Lds L;
   size_t o = 0;
-  const bool codes = part != 1 || mode == kModeTrue;  // true scores: the top-k values or the gather
-  const bool apx = part != 2;                         // approximate scores
   L.mx = o;
-  if (codes) o += r2_al16((size_t)T * kst);
+  o += r2_al16((size_t)T * kst);
   L.sT = o;
-  if (codes) o += r2_al16((size_t)T * nbd * 2);
-  L.op = o;
-  if (apx && (mode == kModeOpExp || mode == kModeOpMul)) o += r2_al16((size_t)T * kst);
-  L.sA = o;
-  if (apx && mode != kModeTrue) o += r2_al16((size_t)T * nbd * 2);
-  L.sg = o;
-  if (apx && mode == kModeExSign) o += r2_al16((size_t)T * nbd * 4);
+  o += r2_al16((size_t)T * nbd * 2);
   L.vt = o;
-  if (part != 1) o += r2_al16((size_t)D * vst);
+  o += r2_al16((size_t)D * vst);
   L.vs = o;
-  if (part != 1) o += r2_al16((size_t)ntb * D * 2);
+  o += r2_al16((size_t)ntb * D * 2);
   L.waves = o;
-  // top-k scratch (mxa_topk_lds.hpp layout), the P code row, P block exponents
-  // and block maxima (16 each)
-  L.per_wave = part != 1 ? r2_al16((size_t)tpad) + 64 + 64 : 0;
+  L.per_wave = r2_al16((size_t)tpad) + 64 + 64;
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
@@ -116,64 +105,41 @@ __device__ __forceinline__ double r2_dot(const int8_t* qrow, const int16_t* qs, 
   return acc;
 }
 
-// PART 0: the dense branch (top_k=False: softmax over every key); PART 2: the
-// finishing kernel of the top-k path (the kept indices come from select_kernel)
-template <int S, int MODE, bool TOPK, bool BIG, int PART>
-__global__ __launch_bounds__(1024, 1) void attn_rows2_kernel(Rows2Args a) {
-  static_assert(PART == 0 || PART == 2, "part 1 is select_kernel (mxa_select.hpp)");
+template <int S>
+__global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x;
   const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, vst = a.vst, ntb = a.ntb;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const Rows2Lds L = rows2_lds(MODE, T, D, kst, nbd, vst, ntb, S, a.tpad, TOPK ? a.k_top : 0, a.waves, PART);
-  constexpr bool kCodes = PART != 1 || MODE == kModeTrue, kApx = PART != 2, kFin = PART != 1;
+  const Rows2Lds L = rows2_lds(T, D, kst, nbd, vst, ntb, a.tpad, a.waves);
   int8_t* tmx = reinterpret_cast<int8_t*>(smem + L.mx);
   int16_t* tsT = reinterpret_cast<int16_t*>(smem + L.sT);
-  int8_t* top = reinterpret_cast<int8_t*>(smem + L.op);
-  int16_t* tsA = reinterpret_cast<int16_t*>(smem + L.sA);
-  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
   int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
   int16_t* tvs = reinterpret_cast<int16_t*>(smem + L.vs);
   unsigned char* wbase = smem + L.waves + (size_t)wave * L.per_wave;
   int8_t* prow = reinterpret_cast<int8_t*>(wbase);
   int* pe = reinterpret_cast<int*>(wbase + r2_al16(a.tpad));
-  uint32_t* bm = reinterpret_cast<uint32_t*>(pe + 16);
 
   // ---- stage the head's K and V tables ---------------------------------------
   const int64_t kb = (int64_t)bh * T;
   {
     const int cpr = a.dpad / 16;
-    if (kCodes || (kOp && kApx)) {
-      for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
-        const int j = i / cpr, c = i - j * cpr;
-        if (kCodes)
-          *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
-              *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
-        if (kOp && kApx)
-          *reinterpret_cast<uint4*>(top + (size_t)j * kst + 16 * c) =
-              *reinterpret_cast<const uint4*>(a.kop + (kb + j) * a.dpad + 16 * c);
-      }
+    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+      const int j = i / cpr, c = i - j * cpr;
+      *reinterpret_cast<uint4*>(tmx + (size_t)j * kst + 16 * c) =
+          *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
     }
-    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      if (kCodes) tsT[i] = a.ksT[kb * nbd + i];
-      if (kApx && MODE != kModeTrue) tsA[i] = a.ksA[kb * nbd + i];
-      if (kApx && MODE == kModeExSign) tsg[i] = a.ksg[kb * nbd + i];
+    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tsT[i] = a.ksT[kb * nbd + i];
+    const int vpr = a.tpad / 16;
+    const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
+    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
+      const int d = i / vpr, c = i - d * vpr;
+      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
+          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
     }
-    if (kFin) {
-      const int vpr = a.tpad / 16;
-      const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
-      for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
-        const int d = i / vpr, c = i - d * vpr;
-        *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
-            *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
-      }
-      const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
-      for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];
-      for (int c = lane; c < a.tpad / 4; c += 64) reinterpret_cast<uint32_t*>(prow)[c] = 0u;
-      if (lane < 16) bm[lane] = 0u;
-    }
+    const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
+    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];
   }
   __syncthreads();
 
@@ -181,187 +147,63 @@ __global__ __launch_bounds__(1024, 1) void attn_rows2_kernel(Rows2Args a) {
   for (int r = (int)blockIdx.y * a.rows_per_wg + __builtin_amdgcn_readfirstlane(wave); r < r_end; r += a.waves) {
     const int64_t grow = (int64_t)bh * a.N + r;
     const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
-
     const int8_t* qmx = a.qc + grow * a.dpad;
 
-    // ---- the row's T values in position order ------------------------------
+    // ---- the row's T true scores in position order ----------------------------
     float vals[S];
-    if constexpr (PART != 2) {
-    if constexpr (MODE == kModeExSign) {
-      // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
-      uint32_t sq[kMaxNB];
-      int eq[kMaxNB];
 #pragma unroll
-      for (int b = 0; b < kMaxNB; ++b) {
-        sq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
-        eq[b] = b < nbd ? s_exp16(a.qsA, grow * nbd + b) : 0;
-      }
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = min(64 * s + lane, T - 1);  // clamped: no exec branch (positions >= T are never ranked)
-        double acc = 0.0;
-        bool nan = false;
-#pragma unroll
-        for (int b = 0; b < kMaxNB; ++b) {
-          if (b < nbd) {
-            const int e = exp_from16(tsA[j * nbd + b]);
-            nan = nan || e == kExpNaN || eq[b] == kExpNaN;
-            const int m = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
-            acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
-          }
-        }
-        vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
-      }
-    } else if constexpr (kOp) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = min(64 * s + lane, T - 1);
-        bool nan = false;
-        const double acc = r2_dot<MODE == kModeOpMul>(a.qop + grow * a.dpad, a.qsA, grow * nbd, nbd, top + (size_t)j * kst, tsA + j * nbd, nan);
-        vals[s] = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = min(64 * s + lane, T - 1);
-        bool nan = false;
-        const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
-        // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
-        vals[s] = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
-      }
+    for (int s = 0; s < S; ++s) {
+      const int j = min(64 * s + lane, T - 1);  // clamped: no exec branch
+      bool nan = false;
+      const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
+      // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
+      vals[s] = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int j = 64 * s + lane;
       if (j < T) {
         if (brow) vals[s] = vals[s] + brow[(int64_t)j * a.bs3];
-        if (MODE == kModeTrue) {
-          if (a.true_out) a.true_out[grow * T + j] = vals[s];
-        } else if (a.pred_out) {
-          a.pred_out[grow * T + j] = vals[s];
-        }
-      }
-    }
-    }  // PART != 2
-
-    // the true score of key j for this row (bias included)
-    auto true_of = [&](int j, bool& nan) -> float {
-      const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
-      float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
-      if (brow) t = t + brow[(int64_t)j * a.bs3];
-      return t;
-    };
-    if (kFin && MODE != kModeTrue && a.true_out) {  // debug output: every key's true score
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int j = 64 * s + lane;
-        bool nan = false;
-        const float t = true_of(min(j, T - 1), nan);
-        if (j < T) a.true_out[grow * T + j] = t;
+        if (a.true_out) a.true_out[grow * T + j] = vals[s];
       }
     }
 
-    int ix[S];
-    bool kept[S];
-    if constexpr (TOPK) {
-      static_assert(PART == 2, "top-k rows are selected by select_kernel (mxa_select.hpp)");
+    // ---- attn = softmax(true) over every key ------------------------------------
+    float mx = -INFINITY;
 #pragma unroll
-      for (int s = 0; s < S; ++s) {  // the kept indices of the selection kernel
-        const int pos = 64 * s + lane;
-        kept[s] = pos < a.k_top;
-        ix[s] = kept[s] ? a.idx32[grow * a.k_top + pos] : 0;
-      }
-      // ---- vals = true.gather(idx); softmax ----------------------------------
-      float v[S];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        v[s] = -INFINITY;
-        if (64 * s < a.k_top) {
-          if (kept[s]) {
-            bool nan = false;
-            v[s] = true_of(ix[s], nan);
-            mx = fmaxf(mx, v[s]);
-          }
-        }
-      }
-      mx = wave_max_f32(mx);
-      float sum = 0.0f;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        v[s] = kept[s] ? expf(v[s] - mx) : 0.0f;
-        sum += v[s];
-      }
-      sum = wave_sum_f32(sum);
-      // ---- zeros.scatter_(idx, softmax) -> MXINT8 along keys ------------------
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (kept[s]) {
-          v[s] = round_bfloat(v[s] / sum, a.bfloat, kRoundNearest, 1);
-          atomicMax(&bm[ix[s] >> 5], __float_as_uint(v[s]) & 0x7FFFFFFFu);
-        }
-      }
-      wave_lds_sync();
-      if (lane < ntb) {
-        int e_raw;
-        const int es = scale_exponent(bm[lane], 127, &e_raw);
-        const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
-        pe[lane] = es == kExpNaN ? kExpNaN : es - 6;
-        bm[lane] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);  // 0: NaN block
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (kept[s]) {
-          const uint32_t e = bm[ix[s] >> 5];
-          int code = 0;
-          if (e & 0xFFFFu) {
-            const int es = (int)(e & 0xFFFFu) - 1024;
-            const float x = (e & 0x10000u) ? v[s] * 0.0f : v[s];
-            code = (int)round_code(x, es, 8, kRoundNearest);
-          }
-          prow[ix[s]] = (int8_t)code;
-        }
-      }
-      wave_lds_sync();
-      if (lane < 16) bm[lane] = 0u;
-    } else {
-      // ---- dense: attn = softmax(true) over every key (blocks excluded from top-k)
-      float mx = -INFINITY;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = 64 * s + lane;
-        if (pos >= T) vals[s] = -INFINITY;
-        mx = fmaxf(mx, vals[s]);
-      }
-      mx = wave_max_f32(mx);
-      float sum = 0.0f;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = 64 * s + lane;
-        vals[s] = pos < T ? expf(vals[s] - mx) : 0.0f;
-        sum += vals[s];
-      }
-      sum = wave_sum_f32(sum);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = s * 64 + lane;
-        if (s * 64 >= a.tpad) break;
-        const float x = round_bfloat(vals[s] / sum, a.bfloat, kRoundNearest, 1);
-        const uint32_t mb = half_reduce(__float_as_uint(x) & 0x7FFFFFFFu,
-                                        [](uint32_t u, uint32_t w) { return u > w ? u : w; });
-        int e_raw;
-        const int es = scale_exponent(mb, 127, &e_raw);
-        float xv = x;
-        if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
-        const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
-        if (pos < a.tpad) {
-          prow[pos] = (int8_t)code;
-          if ((lane & 31) == 0) pe[pos >> 5] = es == kExpNaN ? kExpNaN : es - 6;
-        }
-      }
-      wave_lds_sync();
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      if (pos >= T) vals[s] = -INFINITY;
+      mx = fmaxf(mx, vals[s]);
     }
+    mx = wave_max_f32(mx);
+    float sum = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = 64 * s + lane;
+      vals[s] = pos < T ? expf(vals[s] - mx) : 0.0f;
+      sum += vals[s];
+    }
+    sum = wave_sum_f32(sum);
+    // ---- MX(P) along keys: one 32-block per half-wave ----------------------------
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int pos = s * 64 + lane;
+      if (s * 64 >= a.tpad) break;
+      const float x = round_bfloat(vals[s] / sum, a.bfloat, kRoundNearest, 1);
+      const uint32_t mb = half_reduce(__float_as_uint(x) & 0x7FFFFFFFu,
+                                      [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+      int e_raw;
+      const int es = scale_exponent(mb, 127, &e_raw);
+      float xv = x;
+      if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
+      const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+      if (pos < a.tpad) {
+        prow[pos] = (int8_t)code;
+        if ((lane & 31) == 0) pe[pos >> 5] = es == kExpNaN ? kExpNaN : es - 6;
+      }
+    }
+    wave_lds_sync();
 
     // ---- out = MX(P) @ MX(V): v_dot4 over 16 keys per read, fp64 block epilogue
     {
@@ -403,15 +245,7 @@ __global__ __launch_bounds__(1024, 1) void attn_rows2_kernel(Rows2Args a) {
         }
       }
     }
-    // ---- restore the all-zero P row for the next query row ------------------
     wave_lds_sync();
-    if constexpr (TOPK) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int pos = 64 * s + lane;
-        if (64 * s < a.k_top && pos < a.k_top) prow[ix[s]] = 0;
-      }
-    }
   }
 }
 

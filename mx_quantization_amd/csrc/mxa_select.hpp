@@ -1,18 +1,24 @@
 // Selection kernel: approximate scores + exact-order top-k, FOUR query rows per wave.
 //
-// Per workgroup (one head, a chunk of its query rows): the head's score tables
-// (ex_pred: sign words + block exponents; MXINT4 / EXION / partial: approximator
-// codes + block scales; true scores: MXINT8 codes + exponents) are staged in LDS
-// once.  Per wave, four rows at a time, one 16-lane DPP row each:
+// Per workgroup (one head, a chunk of its query rows): the head's score tables are
+// staged in LDS once (sel_lds):
+//   ex_pred        sign words + block exponents
+//   MXINT4 / EXION / partial_*   approximator codes + block scales
+//   true_ex        power-of-two codes + zero indicators + block exponents
+//   ELSA           hash words + the (D+1)-entry cosine table
+//   approx off     MXINT8 codes + exponents (the true scores are ranked)
+// Per wave, four rows at a time, one 16-lane DPP row each:
 //   1. lane gl computes the scores of keys gl, gl + 16, ... into the row's LDS mirror
 //      (exact fp64 block epilogue: the scores are exact sums of integer * 2^e,
 //      SURVEY.md F6), bias added in fp32 as the caller does;
 //   2. grp_topk (mxa_topk_grp.hpp) reproduces torch's CPU topk index order;
-//   3. the k kept indices go out as int64 (the op's idx) and int32 (the finishing
-//      kernel's input), four consecutive rows per wave: contiguous stores.
+//   3. the four rows' kept indices go out as int64 (the op's idx) and int32 (the
+//      finishing kernel's input) in 16-B stores over the rows' contiguous span (whole
+//      128-B lines), and the prune-mask words when asked for.
+// k_top == 0: scores only (mxa_approx_scores).
 // Callers replaced: the approximator + torch.topk of
 //   workloads/deit/scripts/main.py:101-123, workloads/DiT/models.py:168-194,
-//   workloads/PixArt/models/MX_transformer_block.py:660-678, :805-825.
+//   workloads/PixArt/models/MX_transformer_block.py:656-678, :805-825.
 #pragma once
 #include "mxa_topk_grp.hpp"
 
@@ -20,6 +26,42 @@ namespace mxa {
 
 constexpr int kSelWaves = 4;  // waves per workgroup
 constexpr int kSelRows = 32;  // query rows per workgroup (a multiple of 4 * kSelWaves)
+
+// LDS layout of the score tables (then the per-row top-k areas)
+struct SelLds {
+  size_t cd, ex, sg, z, cs, rows;
+};
+__host__ __device__ inline SelLds sel_lds(int mode, int T, int D, int kst, int nbd) {
+  SelLds L;
+  size_t o = 0;
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const bool codes = mode == kModeTrue || mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx;
+  L.cd = o;
+  if (codes) o += al((size_t)T * kst);
+  L.ex = o;
+  if (mode != kModeElsa) o += al((size_t)T * nbd * 2);
+  L.sg = o;
+  if (mode == kModeExSign || mode == kModeElsa) o += al((size_t)T * nbd * 4);
+  L.z = o;
+  if (mode == kModeTrueEx) o += al((size_t)T * kst);
+  L.cs = o;
+  if (mode == kModeElsa) o += al((size_t)(D + 1) * 4);
+  L.rows = o;
+  return L;
+}
+
+__device__ __forceinline__ int dot32(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+  int I = 0;
+  I = __builtin_amdgcn_sdot4((int)a0.x, (int)b0.x, I, false);
+  I = __builtin_amdgcn_sdot4((int)a0.y, (int)b0.y, I, false);
+  I = __builtin_amdgcn_sdot4((int)a0.z, (int)b0.z, I, false);
+  I = __builtin_amdgcn_sdot4((int)a0.w, (int)b0.w, I, false);
+  I = __builtin_amdgcn_sdot4((int)a1.x, (int)b1.x, I, false);
+  I = __builtin_amdgcn_sdot4((int)a1.y, (int)b1.y, I, false);
+  I = __builtin_amdgcn_sdot4((int)a1.z, (int)b1.z, I, false);
+  I = __builtin_amdgcn_sdot4((int)a1.w, (int)b1.w, I, false);
+  return I;
+}
 
 // MX dot product of a query row (codes in registers, two uint4 per 32-block, block
 // exponents qe) with key row krow of the LDS code table: exact block sums by v_dot4,
@@ -33,16 +75,7 @@ __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd,
     if (b < nbd) {
       const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
       const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
-      const uint4 q0 = qv[2 * b], q1 = qv[2 * b + 1];
-      int I = 0;
-      I = __builtin_amdgcn_sdot4((int)q0.x, (int)x0.x, I, false);
-      I = __builtin_amdgcn_sdot4((int)q0.y, (int)x0.y, I, false);
-      I = __builtin_amdgcn_sdot4((int)q0.z, (int)x0.z, I, false);
-      I = __builtin_amdgcn_sdot4((int)q0.w, (int)x0.w, I, false);
-      I = __builtin_amdgcn_sdot4((int)q1.x, (int)x1.x, I, false);
-      I = __builtin_amdgcn_sdot4((int)q1.y, (int)x1.y, I, false);
-      I = __builtin_amdgcn_sdot4((int)q1.z, (int)x1.z, I, false);
-      I = __builtin_amdgcn_sdot4((int)q1.w, (int)x1.w, I, false);
+      const int I = dot32(qv[2 * b], qv[2 * b + 1], x0, x1);
       const int e = exp_from16(kexp[b]);
       if (e == kExpNaN || qe[b] == kExpNaN) nan = true;
       else if (MUL) acc += (double)I * (double)(qe[b] * e) * (1.0 / 4096.0);
@@ -52,41 +85,112 @@ __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd,
   return acc;
 }
 
+// true_ex: a = c * 2^e + z per element (c the power-of-two code, 0 for a zero MX
+// element; z = 1 for a zero element), so per block
+//   sum aQ aK = 2^(eq+ek) <cq,ck> + 2^eq <cq,zk> + 2^ek <zq,ck> + <zq,zk>   (exact in fp64)
+__device__ __forceinline__ double g_dot_trueex(const uint4* qv, const uint4* qz, const int* qe, int nbd,
+                                               const int8_t* krow, const int8_t* kzrow, const int16_t* kexp,
+                                               bool& nan) {
+  double acc = 0.0;
+#pragma unroll
+  for (int b = 0; b < kMaxNB; ++b) {
+    if (b < nbd) {
+      const uint4 k0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
+      const uint4 k1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
+      const uint4 z0 = *reinterpret_cast<const uint4*>(kzrow + 32 * b);
+      const uint4 z1 = *reinterpret_cast<const uint4*>(kzrow + 32 * b + 16);
+      const int I1 = dot32(qv[2 * b], qv[2 * b + 1], k0, k1);
+      const int I2 = dot32(qv[2 * b], qv[2 * b + 1], z0, z1);
+      const int I3 = dot32(qz[2 * b], qz[2 * b + 1], k0, k1);
+      const int I4 = dot32(qz[2 * b], qz[2 * b + 1], z0, z1);
+      const int e = exp_from16(kexp[b]);
+      if (e == kExpNaN || qe[b] == kExpNaN) {
+        nan = true;
+      } else {
+        acc += (double)I1 * pow2d(qe[b] + e);
+        acc += (double)I2 * pow2d(qe[b]);
+        acc += (double)I3 * pow2d(e);
+        acc += (double)I4;
+      }
+    }
+  }
+  return acc;
+}
+
+// ELSA cosine table entry h: cos(clamp(fl32(fl32(pi/D) * h) - 0.127f, 0)) correctly
+// rounded (funcs/elsa_approximation.py:138-143; the caller may pass torch's values)
+__device__ __forceinline__ float elsa_cos_entry(int D, int h) {
+  const float est = (float)(3.141592653589793 / (double)D) * (float)h;
+  const float cor = fmaxf(est - 0.127f, 0.0f);
+  return (float)cos((double)cor);
+}
+
+// 16-B stores of cnt values val(f) at dst[0..cnt) (lane-strided, whole lines where
+// the span covers them); W = values per 16 B
+template <int W, typename Tv, typename F>
+__device__ __forceinline__ void store_span(Tv* dst, int cnt, int lane, F val) {
+  const int off = (int)(((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(Tv));
+  if (lane < min(off, cnt)) dst[lane] = val(lane);
+  for (int f = off + W * lane; f < cnt; f += 64 * W) {
+    if (f + W <= cnt) {
+      if constexpr (W == 2) {
+        const uint64_t v0 = (uint64_t)val(f), v1 = (uint64_t)val(f + 1);
+        *reinterpret_cast<uint4*>(dst + f) = make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
+      } else {
+        *reinterpret_cast<uint4*>(dst + f) =
+            make_uint4((uint32_t)val(f), (uint32_t)val(f + 1), (uint32_t)val(f + 2), (uint32_t)val(f + 3));
+      }
+    } else {
+      for (int w = 0; w < cnt - f; ++w) dst[f + w] = val(f + w);
+    }
+  }
+}
+
 template <int NP, int MODE>
 __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
   const int bh = blockIdx.x;
-  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst;
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const Rows2Lds L = rows2_lds(MODE, T, D, kst, nbd, a.vst, a.ntb, 1, a.tpad, 0, 0, 1);
-  int8_t* tcd = reinterpret_cast<int8_t*>(smem + (MODE == kModeTrue ? L.mx : L.op));  // key codes
-  int16_t* tex = reinterpret_cast<int16_t*>(smem + (MODE == kModeTrue ? L.sT : L.sA));  // key exponents
-  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
+  const SelLds L = sel_lds(MODE, T, D, kst, nbd);
+  int8_t* tcd = reinterpret_cast<int8_t*>(smem + L.cd);    // key codes
+  int16_t* tex = reinterpret_cast<int16_t*>(smem + L.ex);  // key exponents
+  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);  // sign / hash words
+  int8_t* tz = reinterpret_cast<int8_t*>(smem + L.z);      // true_ex zero indicators
+  float* tcs = reinterpret_cast<float*>(smem + L.cs);      // ELSA cosine table
 
   // ---- stage the head's score tables ----------------------------------------
   const int64_t kb = (int64_t)bh * T;
-  if constexpr (MODE == kModeTrue || kOp) {
+  if constexpr (MODE == kModeTrue || kOp || MODE == kModeTrueEx) {
     const int8_t* src = MODE == kModeTrue ? a.kc : a.kop;
     const int cpr = a.dpad / 16;
     for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
       const int j = i / cpr, c = i - j * cpr;
       *reinterpret_cast<uint4*>(tcd + (size_t)j * kst + 16 * c) =
           *reinterpret_cast<const uint4*>(src + (kb + j) * a.dpad + 16 * c);
+      if (MODE == kModeTrueEx)
+        *reinterpret_cast<uint4*>(tz + (size_t)j * kst + 16 * c) =
+            *reinterpret_cast<const uint4*>(a.kz + (kb + j) * a.dpad + 16 * c);
     }
   }
   {
     const int16_t* esrc = MODE == kModeTrue ? a.ksT : a.ksA;
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      tex[i] = esrc[kb * nbd + i];
-      if (MODE == kModeExSign) tsg[i] = a.ksg[kb * nbd + i];
+      if (MODE != kModeElsa) tex[i] = esrc[kb * nbd + i];
+      if (MODE == kModeExSign || MODE == kModeElsa) tsg[i] = a.ksg[kb * nbd + i];
     }
+    if (MODE == kModeElsa)
+      for (int h = threadIdx.x; h <= D; h += blockDim.x) tcs[h] = a.elsa_cos ? a.elsa_cos[h] : elsa_cos_entry(D, h);
   }
   __syncthreads();
 
   const int npa = grp_alloc(T);
-  const GrpRow g = carve_grp(smem + L.waves + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
+  const size_t rowb = grp_row_bytes(npa, NP);
+  unsigned char* wrows = smem + L.rows + (size_t)(4 * wave) * rowb;  // the wave's four row areas
+  const GrpRow g = carve_grp(wrows + (size_t)gi * rowb, npa, NP);
+  const int ntw = (T + 31) / 32;  // prune-mask words per row
   const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
   for (int rq = (int)blockIdx.y * a.rows_per_wg + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
     const int r = rq + gi;
@@ -96,6 +200,15 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
 
     // ---- the row's scores into its mirror ------------------------------------
     if (valid) {
+      auto emit = [&](int j, float v) {
+        if (brow) v = v + brow[(int64_t)j * a.bs3];
+        if (MODE == kModeTrue) {
+          if (a.true_out) a.true_out[grow * T + j] = v;
+        } else if (a.pred_out) {
+          a.pred_out[grow * T + j] = v;
+        }
+        g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+      };
       if constexpr (MODE == kModeExSign) {
         // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
         uint32_t sq[kMaxNB];
@@ -117,50 +230,80 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
               acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
             }
           }
-          float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
-          if (brow) v = v + brow[(int64_t)j * a.bs3];
-          if (a.pred_out) a.pred_out[grow * T + j] = v;
-          g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+          emit(j, nan ? __uint_as_float(0x7FC00000u) : (float)acc);
+        }
+      } else if constexpr (MODE == kModeElsa) {
+        // approx = ||MX_K[row r]|| * cos(clamp(pi/D * hamming - 0.127, 0))
+        // (elsa_approximation.py:124-143; the key norm of row r, the reference's broadcast)
+        uint32_t hq[kMaxNB];
+#pragma unroll
+        for (int b = 0; b < kMaxNB; ++b) hq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
+        const float nrm = a.knorm[kb + r];
+        for (int j = gl; j < T; j += 16) {
+          int h = 0;
+#pragma unroll
+          for (int b = 0; b < kMaxNB; ++b)
+            if (b < nbd) h += (int)__popc(hq[b] ^ tsg[j * nbd + b]);
+          emit(j, nrm * tcs[h]);
         }
       } else {
         const int8_t* qsrc = (MODE == kModeTrue ? a.qc : a.qop) + grow * a.dpad;
         const int16_t* qesrc = (MODE == kModeTrue ? a.qsT : a.qsA) + grow * nbd;
         uint4 qv[2 * kMaxNB];
+        uint4 qz[MODE == kModeTrueEx ? 2 * kMaxNB : 1];
         int qe[kMaxNB];
 #pragma unroll
         for (int b = 0; b < kMaxNB; ++b) {
           qv[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b) : make_uint4(0, 0, 0, 0);
           qv[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
+          if constexpr (MODE == kModeTrueEx) {
+            const int8_t* zsrc = a.qz + grow * a.dpad;
+            qz[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b) : make_uint4(0, 0, 0, 0);
+            qz[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
+          }
           qe[b] = b < nbd ? exp_from16(qesrc[b]) : 0;
         }
         for (int j = gl; j < T; j += 16) {
           bool nan = false;
-          const double acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
+          double acc;
+          if constexpr (MODE == kModeTrueEx)
+            acc = g_dot_trueex(qv, qz, qe, nbd, tcd + (size_t)j * kst, tz + (size_t)j * kst, tex + j * nbd, nan);
+          else
+            acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
           float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
           // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
           if (MODE == kModeTrue) v = round_bfloat(v, a.bfloat, kRoundNearest, 1) * a.scale;
-          if (brow) v = v + brow[(int64_t)j * a.bs3];
-          if (MODE == kModeTrue) {
-            if (a.true_out) a.true_out[grow * T + j] = v;
-          } else if (a.pred_out) {
-            a.pred_out[grow * T + j] = v;
-          }
-          g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+          emit(j, v);
         }
       }
     }
+    if (k <= 0) continue;  // scores only
     wave_lds_sync();
 
     // ---- torch CPU top-k order ------------------------------------------------
-    grp_topk<NP>(g, T, a.k_top, valid, gl);
+    grp_topk<NP>(g, T, k, valid, gl);
 
-    // ---- kept indices: four consecutive rows per wave ----------------------------
-    if (valid) {
-      for (int p = gl; p < a.k_top; p += 16) {
-        const uint32_t ix = (uint32_t)g.A[p];
-        if (a.idx_out) a.idx_out[grow * a.k_top + p] = (int64_t)ix;
-        a.idx32[grow * a.k_top + p] = (int32_t)ix;
-      }
+    // ---- kept indices of the wave's rows: one contiguous span each ----------------
+    const int nv = min(4, r_end - rq);
+    const int64_t g0 = (int64_t)bh * a.N + rq;
+    auto kept = [&](int f) -> uint32_t {  // f-th index of the span: row f / k, slot f % k
+      const int ri = (f >= k) + (f >= 2 * k) + (f >= 3 * k);
+      return (uint32_t)*(const lu32*)(wrows + (size_t)ri * rowb + (size_t)8 * (f - ri * k));
+    };
+    if (a.idx_out) store_span<2>(a.idx_out + g0 * k, nv * k, lane, [&](int f) { return (int64_t)kept(f); });
+    store_span<4>(a.idx32 + g0 * k, nv * k, lane, [&](int f) { return (int32_t)kept(f); });
+    if (a.mask_out) {  // prune mask: zeros.scatter_(-1, idx, 1) as bits
+      lu32* mw = g.stk;  // free after grp_topk
+      if (gl < ntw) mw[gl] = 0u;
+      wave_lds_sync();
+      if (valid)
+        for (int p = gl; p < k; p += 16) {
+          const uint32_t ix = (uint32_t)g.A[p];
+          atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
+        }
+      wave_lds_sync();
+      if (valid)
+        for (int w = gl; w < ntw; w += 16) a.mask_out[grow * ntw + w] = mw[w];
     }
     wave_lds_sync();
   }
@@ -173,6 +316,7 @@ struct GrpTopkArgs {
   int n, k;
   int64_t* out_idx;
   float* out_vals;
+  uint32_t* out_mask;
 };
 
 template <int NP>
@@ -194,6 +338,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
       a.out_idx[row * a.k + p] = (int64_t)ix;
       if (a.out_vals) a.out_vals[row * a.k + p] = src[ix];
     }
+  }
+  if (a.out_mask) {
+    const int ntw = (a.n + 31) / 32;
+    lu32* mw = g.stk;
+    if (gl < ntw) mw[gl] = 0u;
+    wave_lds_sync();
+    if (valid)
+      for (int p = gl; p < a.k; p += 16) {
+        const uint32_t ix = (uint32_t)g.A[p];
+        atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
+      }
+    wave_lds_sync();
+    if (valid)
+      for (int w = gl; w < ntw; w += 16) a.out_mask[row * ntw + w] = mw[w];
   }
 }
 

@@ -11,6 +11,7 @@ from . import _native as N
 from ._native import check, lib, require_device, stream_ptr
 
 _WS: dict = {}
+_ELSA_COS: dict = {}
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -112,19 +113,28 @@ def approx_values(X: torch.Tensor, kind: str, flush: bool = False, bfloat: int =
     return out
 
 
-def topk(vals: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def topk(vals: torch.Tensor, k: int, return_mask: bool = False):
     """torch.topk(vals, k, dim=-1, largest=True, sorted=True) with torch's CPU
-    index order (TopKImpl.h:45-86), computed on the device."""
+    index order (TopKImpl.h:45-86), computed on the device.  Returns (values, idx),
+    plus the prune mask as packed words (..., ceil(n/32)) int32 if return_mask."""
     dev = require_device(vals)
     vals = _f32(vals, "vals").contiguous()
     n = vals.shape[-1]
     rows = vals.numel() // n if n else 0
     idx = torch.empty(vals.shape[:-1] + (k,), dtype=torch.int64, device=dev)
     out = torch.empty(vals.shape[:-1] + (k,), dtype=torch.float32, device=dev)
-    if rows and k:
-        check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(), stream_ptr(dev)),
-              "mxa_topk")
-    return out, idx
+    mask = torch.empty(vals.shape[:-1] + ((n + 31) // 32,), dtype=torch.int32, device=dev) if return_mask else None
+    if rows:
+        check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(),
+                             mask.data_ptr() if return_mask else None, stream_ptr(dev)), "mxa_topk")
+    return (out, idx, mask) if return_mask else (out, idx)
+
+
+def unpack_mask(words: torch.Tensor, n: int) -> torch.Tensor:
+    """Packed prune-mask words (..., ceil(n/32)) -> bool (..., n) (bit j%32 of word j/32)."""
+    bits = torch.arange(32, device=words.device, dtype=torch.int32)
+    m = (words.unsqueeze(-1) >> bits) & 1
+    return m.reshape(words.shape[:-1] + (-1,))[..., :n].bool()
 
 
 def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbits_b: int = 8, flush: bool = False,
@@ -166,30 +176,38 @@ def _strides3(t: torch.Tensor, name: str):
     return (t.stride(0), t.stride(1), t.stride(2))
 
 
-def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, k_top: int = 20,
-                      pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
-                      bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
-                      return_scores: bool = False, out: Optional[torch.Tensor] = None):
-    """The fused hot path (include/mxa.h mxa_attention): q (B,H,N,D), k/v (B,H,T,D)
-    float32 (strided views of a packed qkv are fine).  Returns (out (B,H,N,D),
-    idx (B,H,N,k_top) int64 or None[, true, pred])."""
-    dev = require_device(q, k, v, bias)
-    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+def elsa_cos_table(d: int) -> torch.Tensor:
+    """cos(clamp(pi/d * h - 0.127, 0)) for hamming distances h = 0..d, computed the way
+    funcs/elsa_approximation.py:138-143 computes it (fp32 torch ops on the host, torch's
+    CPU cosf).  A (d+1)-entry constant of the approximator; the per-pair scores are
+    formed on the device."""
+    h = torch.arange(d + 1, dtype=torch.float32)
+    est = (torch.pi / d) * h
+    return torch.cos(torch.clamp(est - 0.127, min=0))
+
+
+def _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx, bias, flush_subnormals, bfloat, elsa_proj):
+    dev = require_device(q, k, v, bias, elsa_proj)
+    for t, nm in ((q, "q"), (k, "k")) + (((v, "v"),) if v is not None else ()):
         _f32(t, nm)
     B, H, Nq, D = q.shape
     Bk, Hk, T, Dk = k.shape
-    if (Bk, Hk, Dk) != (B, H, D) or tuple(v.shape) != (B, H, T, D):
-        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if (Bk, Hk, Dk) != (B, H, D) or (v is not None and tuple(v.shape) != (B, H, T, D)):
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} "
+                         f"v{None if v is None else tuple(v.shape)}")
     if top_k and not (0 < k_top <= T):
         raise ValueError(f"k={k_top} out of range for {T} keys")
-    if top_k and approx and pred_mode not in N.PRED_MODES:
+    if approx and pred_mode not in N.PRED_MODES:
         raise ValueError(f"pred_mode {pred_mode!r} not supported by the fused op "
                          f"(supported: {sorted(N.PRED_MODES)})")
+    keep = []  # tensors whose storage the call reads
     p = N.AttnParams()
-    p.q, p.k, p.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+    p.q, p.k = q.data_ptr(), k.data_ptr()
+    p.v = v.data_ptr() if v is not None else None
     p.q_strides[:] = _strides3(q, "q")
     p.k_strides[:] = _strides3(k, "k")
-    p.v_strides[:] = _strides3(v, "v")
+    if v is not None:
+        p.v_strides[:] = _strides3(v, "v")
     p.B, p.H, p.N, p.T, p.D = B, H, Nq, T, D
     p.k_top = int(k_top) if top_k else 0
     p.scale = float(torch.tensor(scale, dtype=torch.float32).item())  # torch: python scale -> fp32 operand
@@ -204,6 +222,35 @@ def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: 
         bias4 = bias4.expand(B, H, Nq, T)
         p.bias = bias4.data_ptr()
         p.bias_strides[:] = tuple(bias4.stride())
+    if approx and pred_mode == "ELSA":
+        if elsa_proj is None:
+            raise ValueError("pred_mode 'ELSA' needs the caller's orthogonal matrix (elsa_proj)")
+        if Nq != T:
+            # elsa_approximation.py:142-143 broadcasts the key norms over the query rows
+            raise RuntimeError(f"ELSA scores need N == T (got N={Nq}, T={T}): the reference's key-norm "
+                               f"broadcast (funcs/elsa_approximation.py:142) fails otherwise")
+        proj = _f32(elsa_proj, "elsa_proj").contiguous()
+        if tuple(proj.shape) != (D, D):
+            raise ValueError(f"elsa_proj must be ({D}, {D})")
+        ck = (D, dev)
+        if ck not in _ELSA_COS:
+            _ELSA_COS[ck] = elsa_cos_table(D).to(dev)
+        cos = _ELSA_COS[ck]
+        keep += [proj, cos]
+        p.elsa_proj, p.elsa_cos = proj.data_ptr(), cos.data_ptr()
+    return p, dev, (B, H, Nq, T, D), keep
+
+
+def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, k_top: int = 20,
+                      pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
+                      bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
+                      return_scores: bool = False, out: Optional[torch.Tensor] = None,
+                      return_mask: bool = False, elsa_proj: Optional[torch.Tensor] = None):
+    """The fused hot path (include/mxa.h mxa_attention): q (B,H,N,D), k/v (B,H,T,D)
+    float32 (strided views of a packed qkv are fine).  Returns (out (B,H,N,D),
+    idx (B,H,N,k_top) int64 or None[, true, pred][, mask words (B,H,N,ceil(T/32))])."""
+    p, dev, (B, H, Nq, T, D), keep = _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx and top_k, bias,
+                                                  flush_subnormals, bfloat, elsa_proj)
     if out is None:
         out = torch.empty((B, H, Nq, D), dtype=torch.float32, device=dev)
     p.out = out.data_ptr()
@@ -212,6 +259,12 @@ def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: 
         raise ValueError("out must be contiguous in its last axis")
     idx = torch.empty((B, H, Nq, k_top), dtype=torch.int64, device=dev) if top_k else None
     p.idx_out = idx.data_ptr() if idx is not None else None
+    mask = None
+    if return_mask:
+        if not top_k:
+            raise ValueError("the prune mask exists on the top-k path only")
+        mask = torch.empty((B, H, Nq, (T + 31) // 32), dtype=torch.int32, device=dev)
+        p.mask_out = mask.data_ptr()
     true_s = pred_s = None
     if return_scores:
         true_s = torch.empty((B, H, Nq, T), dtype=torch.float32, device=dev)
@@ -223,9 +276,24 @@ def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: 
     ws = _workspace(dev, nbytes)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
     check(lib().mxa_attention(ctypes.byref(p), stream_ptr(dev)), "mxa_attention")
-    if return_scores:
-        return out, idx, true_s, pred_s
-    return out, idx
+    res = (out, idx) + ((true_s, pred_s) if return_scores else ()) + ((mask,) if return_mask else ())
+    return res
+
+
+def mx_approx_scores(q: torch.Tensor, k: torch.Tensor, pred_mode: str = "ex_pred",
+                     bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
+                     elsa_proj: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """pred = aQ @ aK^T (+ bias) of the approximator `pred_mode` (or ELSA's
+    approximation_scores), (B,H,N,T) float32 -- include/mxa.h mxa_approx_scores."""
+    p, dev, (B, H, Nq, T, D), keep = _attn_params(q, k, None, 1.0, 0, pred_mode, False, True, bias,
+                                                  flush_subnormals, bfloat, elsa_proj)
+    pred = torch.empty((B, H, Nq, T), dtype=torch.float32, device=dev)
+    p.pred_out = pred.data_ptr()
+    nbytes = lib().mxa_attention_workspace_bytes(ctypes.byref(p))
+    ws = _workspace(dev, nbytes)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    check(lib().mxa_approx_scores(ctypes.byref(p), stream_ptr(dev)), "mxa_approx_scores")
+    return pred
 
 
 def selftest_mfma(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -250,7 +250,37 @@ class ExponentApproximation:
         return self._undo(self._true_ex(self.bQ)), self._undo(self._true_ex(self.bK))
 
 
-PRED_MODES = ("ex_pred", "partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex")
+PRED_MODES = ("ex_pred", "partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex", "ELSA")
+
+
+def elsa_cos_table(d):
+    """cos(clamp(fl32(pi/d) * h - 0.127, 0)), h = 0..d: funcs/elsa_approximation.py:138-143
+    evaluated with torch's own fp32 ops (torch.cos on the CPU is not correctly rounded
+    on every entry, and the reference's scores carry its values)."""
+    import torch
+    h = torch.arange(d + 1, dtype=torch.float32)
+    return torch.cos(torch.clamp((torch.pi / d) * h - 0.127, min=0)).numpy()
+
+
+def elsa_scores(Q, K, proj, block_size=32, flush=False, bfloat=32):
+    """elsa_approximation(Q, K).approximation_scores() (funcs/elsa_approximation.py:68-143):
+    MXINT8 of Q, K along d (:83-96); hash bit j = (MX . P[j] >= 0) (:105-112, the
+    products exact in float64); hamming distance over d bits (:128-137); the cosine of
+    the corrected angle from the table above; scaled by ||MX_K[row n]|| for query row n
+    (:126, :142-143: the key norms broadcast over the QUERY axis, so N == T)."""
+    mq = quantize_mx(quantize_bfloat(Q, bfloat), "int8", block_size, -1, flush=flush)[0]
+    mk = quantize_mx(quantize_bfloat(K, bfloat), "int8", block_size, -1, flush=flush)[0]
+    if mq.shape[-2] != mk.shape[-2]:
+        raise RuntimeError("ELSA scores need N == T (elsa_approximation.py:142)")
+    P = np.asarray(proj, F32).astype(F64)
+    with np.errstate(invalid="ignore"):
+        hq = (mq.astype(F64) @ P.T) >= 0
+        hk = (mk.astype(F64) @ P.T) >= 0
+    d = Q.shape[-1]
+    ham = (hq[..., :, None, :] != hk[..., None, :, :]).sum(-1)
+    with np.errstate(invalid="ignore", over="ignore"):
+        knorm = np.sqrt((mk.astype(F64) ** 2).sum(-1)).astype(F32)
+    return (knorm[..., :, None] * elsa_cos_table(d)[ham]).astype(F32)
 
 
 def approx_operands(Q, K, mode, block_size=32, flush=False, bfloat=32):
@@ -338,7 +368,7 @@ def softmax_f32(x, axis=-1):
 # the attention core (caller glue restated)
 # ---------------------------------------------------------------------------
 def attention(q, k, v, scale, k_top=20, pred_mode="ex_pred", top_k=True, approx=True,
-              bias=None, block_size=32, flush=False, bfloat=32):
+              bias=None, block_size=32, flush=False, bfloat=32, elsa_proj=None):
     """The mx_quant branch of QuantizedAttention.forward (deit main.py:100-152) /
     DiT Attention.forward (models.py:168-225) / MXCrossAttention.forward
     (MX_transformer_block.py:792-859), from q,k,v (…,N,d),(…,T,d) to the
@@ -354,7 +384,12 @@ def attention(q, k, v, scale, k_top=20, pred_mode="ex_pred", top_k=True, approx=
         true = (true + bias).astype(F32)
     res["true"] = true
     if top_k:
-        if approx:
+        if approx and pred_mode == "ELSA":
+            pred = elsa_scores(q, k, elsa_proj, block_size, flush=flush, bfloat=bfloat)
+            res["pred"] = pred
+            _, idx = topk(pred, k_top)
+            vals = np.take_along_axis(true, idx, axis=-1)
+        elif approx:
             aq, ak = approx_operands(q, k, pred_mode, block_size, flush=flush, bfloat=bfloat)
             pred = exact_matmul_f32(aq, np.swapaxes(ak, -1, -2))
             if bias is not None:

@@ -35,7 +35,8 @@ import mx  # noqa: E402  (reference)
 from mx.specs import apply_mx_specs  # noqa: E402
 from mx.mx_ops import _quantize_mx, _shared_exponents, _reshape_to_blocks  # noqa: E402
 from mx.elemwise_ops import quantize_elemwise_op  # noqa: E402
-from funcs import exponent_approximation  # noqa: E402  (reference)
+from funcs import exponent_approximation, elsa_approximation  # noqa: E402  (reference)
+from funcs import _create_structured_orthogonal_matrix  # noqa: E402  (reference)
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 torch.set_num_threads(8)
@@ -79,8 +80,10 @@ def approx_ops(q, k, s, mode):
     return getattr(obj, mode)()
 
 
-def attention_glue(q, k, v, s, scale, k_top, mode, top_k=True, approx=True, bias=None):
-    """The mx_quant branch of the patched attention forward (restated)."""
+def attention_glue(q, k, v, s, scale, k_top, mode, top_k=True, approx=True, bias=None, proj=None):
+    """The mx_quant branch of the patched attention forward (restated).  mode 'ELSA'
+    takes the scores from elsa_approximation (orthogonal matrix `proj`), as the
+    modules do (deit main.py:119-121, DiT models.py:187-189, PixArt :675-677)."""
     res = {}
     true_scores = mx.matmul(q, k.transpose(-2, -1), mx_specs=s, mode_config='aa')
     true_scores = true_scores * scale
@@ -88,7 +91,12 @@ def attention_glue(q, k, v, s, scale, k_top, mode, top_k=True, approx=True, bias
         true_scores += bias
     res["true"] = true_scores
     if top_k:
-        if approx:
+        if approx and mode == "ELSA":
+            pred = elsa_approximation(Q=q, K=k, mx_specs=s, orthogonal_matrix=proj).approximation_scores()
+            res["pred"] = pred
+            _, idx = torch.topk(pred, k_top, dim=-1, largest=True, sorted=True)
+            vals = true_scores.gather(dim=-1, index=idx)
+        elif approx:
             aq, ak = approx_ops(q, k, s, mode)
             pred = aq @ ak.transpose(-2, -1)
             if bias is not None:
@@ -171,6 +179,34 @@ def gen_attention():
         pack(store, f"{mode}_k20", r)
     np.savez_compressed(os.path.join(OUT, "attn_pixart_cross.npz"), **store)
     print("wrote attn_pixart_cross")
+
+
+def gen_attention_extra():
+    """attn_extra.npz: ELSA (DeiT-tiny and DiT shapes; the orthogonal matrices made by
+    the reference's _create_structured_orthogonal_matrix under fixed torch seeds, also
+    kept as fixtures of the drop-in's own construction), and the bfloat16 variant
+    (DiT sample.py:42 `bfloat=16`) of ex_pred attention at the DiT shape."""
+    import math
+    store = {}
+    for tag, shape, k_top, seed in (("elsa_deit_k20", (1, 3, 197, 64), 20, 0), ("elsa_dit_k154", (1, 2, 256, 72), 154, 5)):
+        d = shape[-1]
+        torch.manual_seed(100 + d)
+        proj = _create_structured_orthogonal_matrix(d)
+        q, k, v = (torch.from_numpy(rnd(shape, seed + s_)) for s_ in (0, 1, 2))
+        sc = d ** -0.5
+        r = attention_glue(q, k, v, specs(), sc, k_top, "ELSA", proj=proj)
+        store.update({f"{tag}/q": q.numpy(), f"{tag}/k": k.numpy(), f"{tag}/v": v.numpy(), f"{tag}/scale": np.float32(sc),
+                      f"{tag}/proj": proj.numpy(), f"{tag}/proj_seed": np.int64(100 + d), f"{tag}/pred": r["pred"],
+                      f"{tag}/idx": r["idx"], f"{tag}/out": r["out"], f"{tag}/true": r["true"]})
+    # bfloat16 elementwise variant, DiT slice, ex_pred k=154 and the dense branch
+    q, k, v = (torch.from_numpy(rnd((1, 2, 256, 72), 20 + s_)) for s_ in (0, 1, 2))
+    sc = 72 ** -0.5
+    r = attention_glue(q, k, v, specs(bfloat=16), sc, 154, "ex_pred")
+    store.update({"bf16/q": q.numpy(), "bf16/k": k.numpy(), "bf16/v": v.numpy(), "bf16/scale": np.float32(sc),
+                  "bf16/true": r["true"], "bf16/pred": r["pred"], "bf16/idx": r["idx"], "bf16/out": r["out"]})
+    store["bf16/dense_out"] = attention_glue(q, k, v, specs(bfloat=16), sc, 154, "ex_pred", top_k=False)["out"]
+    np.savez_compressed(os.path.join(OUT, "attn_extra.npz"), **store)
+    print("wrote attn_extra")
 
 
 def gen_quant_kat():
@@ -294,6 +330,6 @@ def gen_topk_ties():
 
 
 if __name__ == "__main__":
-    gen_quant_kat()
-    gen_topk_ties()
-    gen_attention()
+    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra"]
+    for w in which:
+        globals()["gen_" + w]()

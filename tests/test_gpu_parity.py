@@ -161,6 +161,17 @@ def test_topk_random_small_alphabets_and_specials(M):
             same(host(idx), want, f"n{n} k{k}")
 
 
+def test_topk_prune_mask_words(M):
+    """mxa_topk's prune-mask output (scatter(1) at idx as bits) on tie-heavy rows."""
+    d = load("topk_ties.npz")
+    for name in ("deit", "dit", "cross"):
+        k = int(d[f"{name}_k"])
+        pred = d[f"{name}_pred"]
+        _, idx, words = M.topk(dev(pred), k, return_mask=True)
+        n = pred.shape[-1]
+        same(host(M.unpack_mask(words, n)), O.prune_mask(d[f"{name}_idx"].astype(np.int64), n), name)
+
+
 @pytest.mark.parametrize("n", [33, 64, 65, 100, 197, 256, 512])
 def test_topk_many_tie_rows(M, n):
     """thousands of rows with heavy ties: every window width of the group partition
@@ -191,6 +202,32 @@ def test_approximator_operands(M, mode):
     same(host(ak)[..., :32, :], d[f"{mode}_k20/ak"], mode + " ak")
 
 
+@pytest.mark.parametrize("mode", ["ex_pred", "partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex"])
+def test_approximator_operands_special_blocks_vs_oracle(M, mode):
+    """NaN / Inf blocks (true_ex maps them to +1 like zeros: examples :98-110), zero
+    elements and rows, tiny and huge block scales, a ragged head dim."""
+    rng = np.random.default_rng(17)
+    q = rng.standard_normal((2, 3, 40, 72), dtype=np.float32)
+    k = rng.standard_normal((2, 3, 40, 72), dtype=np.float32)
+    q[0, 0, 3, 5], q[0, 1, 4, 40], k[1, 2, 6, 70] = np.nan, np.inf, -np.inf
+    q[1, 0, :, ::5] = 0.0
+    k[0, 2, 9, :] = 0.0
+    q[1, 1] *= np.float32(2.0 ** -120)
+    k[1, 1] *= np.float32(2.0 ** 90)
+    M.install_dropin()
+    from funcs import exponent_approximation
+    from mx.specs import apply_mx_specs
+    specs = apply_mx_specs({"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32, "scale_bits": 8,
+                            "bfloat": 32})
+    obj = exponent_approximation(dev(q), dev(k), specs)
+    fn = {"ex_pred": obj.exponent_based_sign, "true_ex": obj.exponent_based_sign_leading_ones}.get(
+        mode, getattr(obj, mode, None))
+    aq, ak = fn()
+    wq, wk = O.approx_operands(q, k, mode)
+    same(host(aq), wq, mode + " aq")
+    same(host(ak), wk, mode + " ak")
+
+
 # ------------------------------------------------------------------ fused attention
 CASES = [
     ("attn_deit_tiny.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
@@ -200,6 +237,7 @@ CASES = [
     ("attn_deit_tiny.npz", "partial_K_k20", dict(pred_mode="partial_K", k_top=20)),
     ("attn_deit_tiny.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20)),
     ("attn_deit_tiny.npz", "two_step_leading_ones_k20", dict(pred_mode="two_step_leading_ones", k_top=20)),
+    ("attn_deit_tiny.npz", "true_ex_k20", dict(pred_mode="true_ex", k_top=20)),
     ("attn_deit_tiny_peaky.npz", "ex_pred_k20", dict(pred_mode="ex_pred", k_top=20)),
     ("attn_dit.npz", "ex_pred_k154", dict(pred_mode="ex_pred", k_top=154)),
     ("attn_pixart_cross.npz", "MXINT4_k20", dict(pred_mode="MXINT4", k_top=20, flush_subnormals=True)),
@@ -213,18 +251,88 @@ CASES = [
 def test_fused_attention_vs_reference(M, fname, tag, kw):
     d = load(fname)
     bias = dev(d["bias"][:, :, None, :]) if "bias" in d.files else None  # (B,1,1,T)
-    out, idx, true_s, pred_s = M.mx_topk_attention(dev(d["q"]), dev(d["k"]), dev(d["v"]), float(d["scale"]),
-                                                   bias=bias, return_scores=True, **kw)
+    topk = kw.get("top_k", True)
+    res = M.mx_topk_attention(dev(d["q"]), dev(d["k"]), dev(d["v"]), float(d["scale"]),
+                              bias=bias, return_scores=True, return_mask=topk, **kw)
+    out, idx, true_s, pred_s = res[:4]
     torch.cuda.synchronize()
     same(host(true_s), d["true"], "true scores")
     if f"{tag}/pred" in d.files:
         same(host(pred_s), d[f"{tag}/pred"], "approx scores")
+        # the scores alone (mxa_approx_scores)
+        alone = M.mx_approx_scores(dev(d["q"]), dev(d["k"]), kw["pred_mode"], bias=bias,
+                                   flush_subnormals=kw.get("flush_subnormals", False))
+        same(host(alone), d[f"{tag}/pred"], "mxa_approx_scores")
     if f"{tag}/idx" in d.files:
         same(host(idx), d[f"{tag}/idx"], "top-k idx")
         T = d["true"].shape[-1]
-        same(O.prune_mask(host(idx), T), O.prune_mask(d[f"{tag}/idx"], T), "prune mask")
+        # the kernel's prune-mask words (mask_out) against scatter(1) at the reference's idx
+        same(host(M.unpack_mask(res[4], T)), O.prune_mask(d[f"{tag}/idx"], T), "prune mask")
     err = O.normwise_rel_err(host(out), d[f"{tag}/out"])
     assert err <= OUT_TOL, err
+
+
+EXTRA = [
+    ("elsa_deit_k20", dict(pred_mode="ELSA", k_top=20)),
+    ("elsa_dit_k154", dict(pred_mode="ELSA", k_top=154)),
+    ("bf16", dict(pred_mode="ex_pred", k_top=154, bfloat=16)),
+]
+
+
+@pytest.mark.parametrize("tag,kw", EXTRA, ids=[t for t, _ in EXTRA])
+def test_fused_attention_extra_vs_reference(M, tag, kw):
+    """ELSA scores (funcs/elsa_approximation.py) and the bfloat16 elementwise variant
+    (DiT sample.py:42) against reference-generated vectors."""
+    d = load("attn_extra.npz")
+    g = lambda n: d[f"{tag}/{n}"]
+    proj = dev(g("proj")) if kw["pred_mode"] == "ELSA" else None
+    out, idx, true_s, pred_s, mask = M.mx_topk_attention(dev(g("q")), dev(g("k")), dev(g("v")), float(g("scale")),
+                                                         return_scores=True, return_mask=True, elsa_proj=proj, **kw)
+    torch.cuda.synchronize()
+    same(host(true_s), g("true"), "true")
+    same(host(pred_s), g("pred"), "pred")
+    same(host(idx), g("idx"), "idx")
+    T = g("true").shape[-1]
+    same(host(M.unpack_mask(mask, T)), O.prune_mask(g("idx"), T), "mask")
+    assert O.normwise_rel_err(host(out), g("out")) <= OUT_TOL
+    if kw["pred_mode"] == "ELSA":  # the drop-in class on the same inputs
+        M.install_dropin()
+        from funcs import elsa_approximation
+        from mx.specs import apply_mx_specs
+        specs = apply_mx_specs({"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32,
+                                "scale_bits": 8, "bfloat": 32})
+        sc = elsa_approximation(Q=dev(g("q")), K=dev(g("k")), mx_specs=specs,
+                                orthogonal_matrix=torch.from_numpy(g("proj"))).approximation_scores()
+        same(host(sc), g("pred"), "elsa_approximation.approximation_scores")
+    else:
+        o2, _ = M.mx_topk_attention(dev(g("q")), dev(g("k")), dev(g("v")), float(g("scale")), top_k=False, bfloat=16)
+        assert O.normwise_rel_err(host(o2), g("dense_out")) <= OUT_TOL
+
+
+@pytest.mark.parametrize("D", [64, 72])
+@pytest.mark.parametrize("mode", ["true_ex", "ELSA"])
+def test_trueex_elsa_vs_oracle(M, mode, D):
+    """true_ex (power-of-two codes + zero indicators) and ELSA (hashes, key norms)
+    against the oracle: odd lengths, zero elements and rows, a NaN row."""
+    rng = np.random.default_rng(D + len(mode))
+    B, H, N = 2, 3, 129
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    q[0, 0, :, ::7] = 0.0          # zero elements (true_ex: exponent 0 -> +1)
+    kk[0, 1, 5, :] = 0.0           # a zero key row (ELSA: zero norm scales query row 5)
+    kk[1, 0, :, 3] *= np.float32(1e-4)
+    q[1, 2, 7, 9] = np.nan
+    proj = None
+    if mode == "ELSA":
+        from mx_quantization_amd.funcs import _create_structured_orthogonal_matrix
+        torch.manual_seed(D)
+        proj = _create_structured_orthogonal_matrix(D).numpy()
+    res = M.mx_topk_attention(dev(q), dev(kk), dev(v), D ** -0.5, k_top=30, pred_mode=mode, return_scores=True,
+                              elsa_proj=None if proj is None else dev(proj))
+    got = [host(t) for t in res]
+    r = O.attention(q, kk, v, D ** -0.5, k_top=30, pred_mode=mode, elsa_proj=proj)
+    _check_vs_oracle(got, r, mode)
 
 
 def test_fused_attention_strided_qkv_views(M):
@@ -255,6 +363,11 @@ def test_fused_attention_full_size_vs_oracle(M, cfg):
     pred_h = host(pred_s)
     _, want = O.topk(pred_h.reshape(-1, N), k)
     same(host(idx).reshape(-1, k), want, "idx (all heads)")
+    # the approximate scores themselves on 16 images spread over the batch
+    imgs = np.linspace(0, B - 1, 16).astype(int)
+    qh, kh = host(q[imgs]), host(kk[imgs])
+    aq, ak = O.approx_operands(qh, kh, "ex_pred")
+    same(pred_h[imgs], O.exact_matmul_f32(aq, np.swapaxes(ak, -1, -2)), "pred (16 images)")
     for b in (0, B // 2, B - 1):
         r = O.attention(host(q[b:b + 1]), host(kk[b:b + 1]), host(v[b:b + 1]), scale, k_top=k)
         same(host(true_s[b:b + 1]), r["true"], "true")
@@ -346,12 +459,12 @@ def test_pixart_cross_full_batch(M):
     kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
     v = rng.standard_normal((B, H, T, D), dtype=np.float32)
     bias = np.where(np.arange(T) < 60, 0.0, -10000.0).astype(np.float32)[None, None, None, :].repeat(B, 0)
-    for mode in ("MXINT4", "two_step_leading_ones"):
+    for mode in ("MXINT4", "two_step_leading_ones", "ex_pred"):
         out, idx = M.mx_topk_attention(dev(q), dev(kk), dev(v), 1 / np.sqrt(72), k_top=k, pred_mode=mode,
                                        bias=dev(bias), flush_subnormals=True)
-        r = O.attention(q[:2], kk[:2], v[:2], 1 / np.sqrt(72), k_top=k, pred_mode=mode, bias=bias[:2], flush=True)
-        same(host(idx)[:2], r["idx"], mode)
-        assert O.normwise_rel_err(host(out)[:2], r["out"]) <= OUT_TOL
+        r = O.attention(q, kk, v, 1 / np.sqrt(72), k_top=k, pred_mode=mode, bias=bias, flush=True)
+        same(host(idx), r["idx"], mode)  # all 8 images
+        assert O.normwise_rel_err(host(out), r["out"]) <= OUT_TOL
 
 
 # ------------------------------------------------------------------ mx.matmul / Linear drop-in

@@ -178,3 +178,40 @@ def test_attention_vs_reference(fname, tag, kw):
         same(O.quantize_mx(d["q"], "int8", 32, -1)[0][..., :64, :], d["mx_q"])
         same(O.quantize_mx(d["k"], "int8", 32, -1)[0][..., :64, :], d["mx_k"])
         same(O.quantize_mx(d["v"], "int8", 32, -2)[0][..., :64, :], d["mx_v"])
+
+
+# ---------------------------------------------------------------- ELSA, bfloat16 (attn_extra.npz)
+EXTRA = [
+    ("elsa_deit_k20", dict(pred_mode="ELSA", k_top=20)),
+    ("elsa_dit_k154", dict(pred_mode="ELSA", k_top=154)),
+    ("bf16", dict(pred_mode="ex_pred", k_top=154, bfloat=16)),
+]
+
+
+@pytest.mark.parametrize("tag,kw", EXTRA, ids=[t for t, _ in EXTRA])
+def test_attention_extra_vs_reference(tag, kw):
+    d = load("attn_extra.npz")
+    g = lambda n: d[f"{tag}/{n}"]
+    proj = g("proj") if kw["pred_mode"] == "ELSA" else None
+    r = O.attention(g("q"), g("k"), g("v"), float(g("scale")), elsa_proj=proj, **kw)
+    same(r["true"], g("true"))
+    same(r["pred"], g("pred"))
+    same(r["idx"], g("idx"))
+    assert O.normwise_rel_err(r["out"], g("out")) <= 1e-3
+    if tag == "bf16":
+        rd = O.attention(g("q"), g("k"), g("v"), float(g("scale")), top_k=False, bfloat=16)
+        assert O.normwise_rel_err(rd["out"], g("dense_out")) <= 1e-3
+
+
+@pytest.mark.parametrize("d", [64, 72])
+def test_dropin_structured_orthogonal_matrix(d):
+    """funcs._create_structured_orthogonal_matrix of the drop-in draws the same
+    torch.randn stream and runs the same modified Gram-Schmidt arithmetic as
+    funcs/elsa_approximation.py:5-58: bit-identical matrices for the same seed."""
+    import torch
+    from mx_quantization_amd.funcs import _create_structured_orthogonal_matrix
+    ex = load("attn_extra.npz")
+    tag = "elsa_deit_k20" if d == 64 else "elsa_dit_k154"
+    torch.manual_seed(int(ex[f"{tag}/proj_seed"]))
+    P = _create_structured_orthogonal_matrix(d).numpy()
+    same(P, ex[f"{tag}/proj"])
