@@ -27,18 +27,18 @@ def _stale(lib=LIB):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True, phase_prof=False):
-    """phase_prof: instrumented build (per-phase cycle counters of the fused
-    kernel, tools/phase_prof.py) into libmxa_prof.so; never the product."""
-    lib = LIB.replace("libmxa.so", "libmxa_prof.so") if phase_prof else LIB
+def build(force=False, verbose=True, defines=(), tag=""):
+    """defines / tag: a tools-only variant (e.g. defines=("MXA_SEL_SKIP=1",), tag="skip1"
+    -> libmxa_skip1.so, loaded by tools through MXA_LIB); never the product."""
+    lib = LIB.replace("libmxa.so", f"libmxa_{tag}.so") if tag else LIB
     if not force and not _stale(lib):
         return lib
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", "_prof.o" if phase_prof else ".o"))
+        obj = os.path.join(CSRC, src.replace(".hip", f"{'_' + tag if tag else ''}.o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                "-Wall", "-Wno-unused-function", "-I", os.path.join(HERE, "..", "include"),
-               "-c", os.path.join(CSRC, src), "-o", obj] + (["-DMXA_PHASE_PROF"] if phase_prof else [])
+               "-c", os.path.join(CSRC, src), "-o", obj] + [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
@@ -54,4 +54,6 @@ def build(force=False, verbose=True, phase_prof=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, phase_prof="--phase-prof" in sys.argv))
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
+    tags = [a[6:] for a in sys.argv[1:] if a.startswith("--tag=")]
+    print(build(force="--force" in sys.argv, defines=defs, tag=tags[0] if tags else ""))

@@ -199,7 +199,11 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
     const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : rq) * a.bs2 : nullptr;
 
     // ---- the row's scores into its mirror ------------------------------------
+#ifdef MXA_SEL_SKIP
+    if (valid && !((MXA_SEL_SKIP) & 2)) {
+#else
     if (valid) {
+#endif
       auto emit = [&](int j, float v) {
         if (brow) v = v + brow[(int64_t)j * a.bs3];
         if (MODE == kModeTrue) {
@@ -277,10 +281,17 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
         }
       }
     }
+#ifdef MXA_SEL_SKIP  // tools-only phase timing (build_native defines): 2 = scores replaced by hashed keys
+    if ((MXA_SEL_SKIP) & 2)
+      for (int j = gl; j < T; j += 16) g.A[j] = pack_ki(0x80000000u | ((uint32_t)(j * 2654435761u + r * 40503u) >> 26), (uint32_t)j);
+#endif
     if (k <= 0) continue;  // scores only
     wave_lds_sync();
 
     // ---- torch CPU top-k order ------------------------------------------------
+#ifdef MXA_SEL_SKIP  // 1 = no top-k
+    if (!((MXA_SEL_SKIP) & 1))
+#endif
     grp_topk<NP>(g, T, k, valid, gl);
 
     // ---- kept indices of the wave's rows: one contiguous span each ----------------
