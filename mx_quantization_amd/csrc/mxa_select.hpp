@@ -12,9 +12,9 @@
 //      (exact fp64 block epilogue: the scores are exact sums of integer * 2^e,
 //      SURVEY.md F6), bias added in fp32 as the caller does;
 //   2. grp_topk (mxa_topk_grp.hpp) reproduces torch's CPU topk index order;
-//   3. the four rows' kept indices go out as int64 (the op's idx) and int32 (the
-//      finishing kernel's input) in 16-B stores over the rows' contiguous span (whole
-//      128-B lines), and the prune-mask words when asked for.
+//   3. the k kept indices go out as int64 (the op's idx) and int32 (the finishing
+//      kernel's input), four consecutive rows per wave, and the prune-mask words
+//      when asked for.
 // k_top == 0: scores only (mxa_approx_scores).
 // Callers replaced: the approximator + torch.topk of
 //   workloads/deit/scripts/main.py:101-123, workloads/DiT/models.py:168-194,
@@ -125,27 +125,6 @@ __device__ __forceinline__ float elsa_cos_entry(int D, int h) {
   return (float)cos((double)cor);
 }
 
-// 16-B stores of cnt values val(f) at dst[0..cnt) (lane-strided, whole lines where
-// the span covers them); W = values per 16 B
-template <int W, typename Tv, typename F>
-__device__ __forceinline__ void store_span(Tv* dst, int cnt, int lane, F val) {
-  const int off = (int)(((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) / sizeof(Tv));
-  if (lane < min(off, cnt)) dst[lane] = val(lane);
-  for (int f = off + W * lane; f < cnt; f += 64 * W) {
-    if (f + W <= cnt) {
-      if constexpr (W == 2) {
-        const uint64_t v0 = (uint64_t)val(f), v1 = (uint64_t)val(f + 1);
-        *reinterpret_cast<uint4*>(dst + f) = make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
-      } else {
-        *reinterpret_cast<uint4*>(dst + f) =
-            make_uint4((uint32_t)val(f), (uint32_t)val(f + 1), (uint32_t)val(f + 2), (uint32_t)val(f + 3));
-      }
-    } else {
-      for (int w = 0; w < cnt - f; ++w) dst[f + w] = val(f + w);
-    }
-  }
-}
-
 template <int NP, int MODE>
 __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -188,8 +167,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
 
   const int npa = grp_alloc(T);
   const size_t rowb = grp_row_bytes(npa, NP);
-  unsigned char* wrows = smem + L.rows + (size_t)(4 * wave) * rowb;  // the wave's four row areas
-  const GrpRow g = carve_grp(wrows + (size_t)gi * rowb, npa, NP);
+  const GrpRow g = carve_grp(smem + L.rows + (size_t)(4 * wave + gi) * rowb, npa, NP);
   const int ntw = (T + 31) / 32;  // prune-mask words per row
   const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
   for (int rq = (int)blockIdx.y * a.rows_per_wg + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
@@ -294,15 +272,16 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
 #endif
     grp_topk<NP>(g, T, k, valid, gl);
 
-    // ---- kept indices of the wave's rows: one contiguous span each ----------------
-    const int nv = min(4, r_end - rq);
-    const int64_t g0 = (int64_t)bh * a.N + rq;
-    auto kept = [&](int f) -> uint32_t {  // f-th index of the span: row f / k, slot f % k
-      const int ri = (f >= k) + (f >= 2 * k) + (f >= 3 * k);
-      return (uint32_t)*(const lu32*)(wrows + (size_t)ri * rowb + (size_t)8 * (f - ri * k));
-    };
-    if (a.idx_out) store_span<2>(a.idx_out + g0 * k, nv * k, lane, [&](int f) { return (int64_t)kept(f); });
-    store_span<4>(a.idx32 + g0 * k, nv * k, lane, [&](int f) { return (int32_t)kept(f); });
+    // ---- kept indices: four consecutive rows per wave ----------------------------
+    // (measured: per-row stores beat 16-B stores over the four rows' span, whose
+    // per-element LDS gathers cost more VALU and whose HBM writes were larger)
+    if (valid) {
+      for (int p = gl; p < k; p += 16) {
+        const uint32_t ix = (uint32_t)g.A[p];
+        if (a.idx_out) a.idx_out[grow * k + p] = (int64_t)ix;
+        a.idx32[grow * k + p] = (int32_t)ix;
+      }
+    }
     if (a.mask_out) {  // prune mask: zeros.scatter_(-1, idx, 1) as bits
       lu32* mw = g.stk;  // free after grp_topk
       if (gl < ntw) mw[gl] = 0u;
