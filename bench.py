@@ -25,7 +25,8 @@ Besides the contract fields the JSON line carries
                 mfma:    Ops_gemm (dense QK^T + PV) over the finishing kernel's time
   cpu_baseline  the CPU oracle (oracle/, test infrastructure) on the host's cores
   parity        top-k index bit-match and output error of a sample of images per rank
-  secondary     the DiT-XL/2 line (the metric names both models) when --config deit_base
+  secondary     the DiT-XL/2 line (the metric names both models) when --config deit_base, and
+                the qkv-Linear-fused line (mxa_qkv_attention) of the config
 """
 from __future__ import annotations
 
@@ -59,6 +60,7 @@ CONFIGS = {
                          B=8, H=16, N=256, T=120, D=72, k=20, mode="MXINT4", scale=1 / np.sqrt(72), bias=True),
 }
 STAGES = ("rows_prep_q", "rows_prep_k", "cols_prep_v", "select", "finish")  # mxa_attention_timed order
+QKV_STAGES = ("-", "x_quant+qkv_proj", "-", "select", "finish")  # mxa_qkv_attention_timed order
 
 
 def stage_bytes(c, path):
@@ -292,6 +294,50 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
     return elapsed, stages, roof, e2e, out, idx
 
 
+def run_qkv(c, images, steps, warmup, device, world):
+    """The qkv mx.Linear fused in front of the attention core (mxa_qkv_attention): x (B, N,
+    H*D) tokens and a (3*H*D, H*D) weight (prepared once, outside the timed region: the
+    weights are constant at inference) -> out + idx.  Returns (elapsed, stage_ms, extra)."""
+    import torch
+    import mx_quantization_amd as M
+    from mx_quantization_amd import _native as N
+    B, H, Nt, D = len(images), c["H"], c["N"], c["D"]
+    C = H * D
+    rng = np.random.default_rng(99)
+    x = torch.from_numpy(rng.standard_normal((B, Nt, C), dtype=np.float32)).to(device)
+    W = torch.from_numpy((rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(C ** -0.5))).to(device)
+    bias = torch.from_numpy(rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.02)).to(device)
+    wq = M.LinearWeightMX(W)
+    for _ in range(max(warmup, 1)):
+        M.mx_qkv_attention(x, wq, bias, H, c["scale"], k_top=c["k"], pred_mode=c["mode"])
+    torch.cuda.synchronize()
+    p = N.AttnParams()
+    p.B, p.H, p.N, p.T, p.D = B, H, Nt, Nt, D
+    p.k_top, p.scale = c["k"], float(np.float32(c["scale"]))
+    p.pred_mode, p.top_k, p.approx = N.PRED_MODES[c["mode"]], 1, 1
+    out = torch.empty((B, H, Nt, D), dtype=torch.float32, device=device)
+    idx = torch.empty((B, H, Nt, c["k"]), dtype=torch.int64, device=device)
+    p.out, p.out_strides[:] = out.data_ptr(), out.stride()[:3]
+    p.idx_out = idx.data_ptr()
+    xp = N.QkvParams()
+    xp.x, xp.x_row_stride, xp.C, xp.wq, xp.bias = x.data_ptr(), C, C, wq.buf.data_ptr(), bias.data_ptr()
+    from mx_quantization_amd.ops import _workspace
+    ws = _workspace(device, N.lib().mxa_qkv_attention_workspace_bytes(ctypes.byref(p), ctypes.byref(xp)))
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    stage_ms = (ctypes.c_float * 5)()
+    stream = torch.cuda.current_stream(device).cuda_stream
+    elapsed = timed_region(
+        lambda: N.check(N.lib().mxa_qkv_attention_timed(ctypes.byref(p), ctypes.byref(xp), stream, steps, stage_ms),
+                        "mxa_qkv_attention_timed"), world, torch.cuda.synchronize, device)
+    stages = {QKV_STAGES[i]: float(stage_ms[i]) for i in range(5) if QKV_STAGES[i] != "-"}
+    proj_ms = stages["x_quant+qkv_proj"]
+    ops = 2 * B * Nt * C * 3 * C  # int8 ops of the projection GEMM
+    extra = {"proj_int8_tops": ops / (proj_ms * 1e-3) / 1e12,
+             "proj_bytes_min": B * Nt * C * 4 + 3 * C * C + B * Nt * C * 3 * 1,
+             "fp32_qkv_bytes_avoided": B * Nt * 3 * C * 4 * 2}
+    return elapsed, stages, extra
+
+
 def launch_ranks(args):
     """--gpus N without WORLD_SIZE: start the N ranks (one process per GPU) through
     torch.distributed.run from this process, which has not touched the GPU, and exit
@@ -392,15 +438,25 @@ def main(argv=None, run=run_config):
                                          torch.cat(gm).cpu().tolist())
             res["parity"]["ranks_checked"] = world
 
+    if args.config in ("deit_base", "dit_xl2") and not args.no_secondary and run is run_config:
+        # the qkv mx.Linear fused in front: x (B, N, C) -> out + idx
+        qsteps = max(args.steps // 2, 1)
+        qel, qst, qex = run_qkv(c, images, qsteps, 2, device, world)
+        qtok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * qsteps
+        res.setdefault("secondary", []).append(
+            {"config": args.config + "+qkv_linear", "workload": "mx.Linear qkv projection (C=%d -> 3C) fused into the "
+             "attention core's MX operands, then the same attention" % (c["H"] * c["D"]),
+             "value": qtok / qel, "unit": "tokens/s", "ms_per_step": qel / qsteps * 1e3, "stages_ms": qst, **qex})
+
     if args.config == "deit_base" and not args.no_secondary:
         d = CONFIGS["dit_xl2"]
         dimg = shard(d, rank, world, args.scaling)
         delapsed, dst, droof, _, _, _ = run(d, dimg, max(args.steps // 2, 1), 2, device, world, None)
         dtok = (world * d["B"] if args.scaling == "weak" else d["B"]) * d["N"] * max(args.steps // 2, 1)
-        res["secondary"] = [{"config": "dit_xl2", "workload": d["workload"], "value": dtok / delapsed,
+        res.setdefault("secondary", []).append({"config": "dit_xl2", "workload": d["workload"], "value": dtok / delapsed,
                              "unit": "tokens/s", "ms_per_step": delapsed / max(args.steps // 2, 1) * 1e3,
                              "batch_per_gpu": len(dimg), "stages_ms": dst,
-                             "roofline_frac": droof["frac"], "qa_pass_frac": droof["qa_pass"]["frac"]}]
+                             "roofline_frac": droof["frac"], "qa_pass_frac": droof["qa_pass"]["frac"]})
 
     if rank == 0:
         print(json.dumps(res), flush=True)

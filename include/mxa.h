@@ -195,6 +195,39 @@ int mxa_attention_path(const mxa_attn_params* p);
 int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms);
 
 /*
+ * The fused MX Linear qkv projection in front of the attention core: the patched
+ * modules' `qkv = self.qkv(x).reshape(B, N, 3, H, D)` (workloads/deit/scripts/main.py:87-88,
+ * workloads/DiT/models.py:156-157) with self.qkv an mx.Linear (microxscaling/mx/linear.py:
+ * 20-103: out = bf(fl32(MX(bf(x)) @ MX(bf(W))^T)); out = bf(out + bf(bias))), feeding the
+ * attention's MX operands directly -- the fp32 q / k / v never reach HBM.
+ *
+ * mxa_linear_weight_prep: W (out_features, in_features) fp32 row-major -> MXINT8 codes +
+ * block exponents along in_features into `wq` (mxa_linear_weight_bytes bytes, 16-B
+ * aligned; once per weight).  out_features = 3 * H * D for the qkv projection.
+ *
+ * mxa_qkv_attention: mxa_attention with q, k, v produced from x (p->q, p->k, p->v are
+ * ignored; self-attention, p->N == p->T).  The projection is exact-then-rounded (the
+ * reference's fp32 GEMM order is unpinned: equal within fp32 rounding).
+ */
+typedef struct mxa_qkv_params {
+  const float* x;        /* (B*N, C) tokens, row stride x_row_stride (elements)            */
+  int64_t x_row_stride;
+  int32_t C;             /* in_features                                                     */
+  const void* wq;        /* mxa_linear_weight_prep output for W (3*H*D, C)                  */
+  const float* bias;     /* (3*H*D) or null                                                 */
+  float* qkv_out;        /* optional (B*N, 3*H*D) fp32 projection (tests)                   */
+} mxa_qkv_params;
+
+int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features);
+int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features, int32_t flush_subnormals,
+                           int32_t bfloat, void* wq, hipStream_t stream);
+int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* x);
+int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream);
+/* mxa_attention_timed for the fused projection path (stage 1 = x quantize + projection) */
+int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream, int32_t iters,
+                            float* stage_ms);
+
+/*
  * mx.matmul forward (microxscaling/mx/matmul.py:31-100, :211-222): in1 (batch, M, K)
  * quantized along K, in2 (batch, K, Nc) quantized along K, fp32 result (batch, M, Nc)
  * contiguous.  Integer formats, block size 32.

@@ -6,6 +6,7 @@ PyTorch-ROCm, exposed through
 
   * `mx_topk_attention` -- the fused path (MXINT8 QK^T, approximate scores,
     exact-order top-k, softmax, MXINT8 P.V),
+  * `mx_qkv_attention` -- the qkv mx.Linear fused in front of it (x -> MX operands),
   * `mx_approx_scores` -- the approximator's scores alone (pred = aQ @ aK^T, ELSA),
   * `topk` -- torch.topk with torch's CPU index order (and the prune mask), on the device,
   * the reference's own operator surface, as drop-in packages:
@@ -19,7 +20,9 @@ from .ops import (  # noqa: F401
     approx_values,
     elsa_cos_table,
     mx_approx_scores,
+    LinearWeightMX,
     mx_matmul,
+    mx_qkv_attention,
     mx_topk_attention,
     quantize_bfloat,
     quantize_mx,
@@ -28,7 +31,7 @@ from .ops import (  # noqa: F401
     unpack_mask,
 )
 
-__all__ = ["mx_topk_attention", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
+__all__ = ["mx_topk_attention", "mx_qkv_attention", "LinearWeightMX", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
 
 
 def install_dropin():

@@ -44,6 +44,12 @@ class AttnParams(ctypes.Structure):
     ]
 
 
+class QkvParams(ctypes.Structure):
+    """mirror of struct mxa_qkv_params (include/mxa.h)"""
+    _fields_ = [("x", c_vp), ("x_row_stride", c_i64), ("C", c_i32), ("wq", c_vp), ("bias", c_vp),
+                ("qkv_out", c_vp)]
+
+
 _SIGS = {
     "mxa_abi_version": (c_i32, []),
     "mxa_status_string": (ctypes.c_char_p, [c_i32]),
@@ -58,6 +64,12 @@ _SIGS = {
     "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_attention_path": (c_i32, [ctypes.POINTER(AttnParams)]),
     "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
+    "mxa_linear_weight_bytes": (c_i64, [c_i32, c_i32]),
+    "mxa_linear_weight_prep": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "mxa_qkv_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams)]),
+    "mxa_qkv_attention": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp]),
+    "mxa_qkv_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp, c_i32,
+                                        ctypes.POINTER(c_f32)]),
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                            c_vp, c_i64, c_vp]),
     "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),

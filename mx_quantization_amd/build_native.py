@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmxa.so")
 SOURCES = ["mxa_quant.hip", "mxa_attn.hip"]
-HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "../../include/mxa.h"]
+HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_finish.hpp", "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -43,6 +43,7 @@ __device__ __forceinline__ int s_exp16(const int16_t* base, int64_t i) {
 
 #include "mxa_rows2.hpp"
 #include "mxa_finish.hpp"
+#include "mxa_proj.hpp"
 
 namespace mxa {
 
@@ -104,7 +105,9 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 // workspace regions, 256-B aligned
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx32, total;
+  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx32;
+  int64_t xc, xs;  // fused qkv projection: x codes / exponents
+  int64_t total;
 };
 
 // the selection kernel's score mode of a call (ranked: the selection kernel runs)
@@ -119,7 +122,7 @@ int score_mode(const mxa_attn_params* p, bool ranked) {
   }
 }
 
-AttnLayout attn_layout(const mxa_attn_params* p, int mode) {
+AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params* xq = nullptr) {
   AttnLayout L{};
   const int64_t BH = (int64_t)p->B * p->H;
   L.nbd = (p->D + 31) / 32;
@@ -153,6 +156,11 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode) {
   L.vt = take(BH * p->D * (int64_t)L.tpad);
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
   L.idx32 = take(p->top_k ? qrows * (int64_t)p->k_top * 4 : 0);
+  if (xq) {
+    const int64_t nbk = (xq->C + 31) / 32, tokens = (int64_t)p->B * p->N;
+    L.xc = take(tokens * nbk * 32);
+    L.xs = take(tokens * nbk * 2);
+  }
   L.total = off;
   return L;
 }
@@ -335,12 +343,69 @@ static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, in
   }
 }
 
+// ---- fused qkv projection (mxa_proj.hpp) ------------------------------------------
+namespace {
+int64_t linear_exps_offset(int32_t out_features, int32_t in_features) {
+  return align_up((int64_t)out_features * ((in_features + 31) / 32) * 32);
+}
+}  // namespace
+
+template <int NBD>
+static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
+  const size_t lds = proj_lds(pa.Cpad, pa.nbk, pa.D).total;
+  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)pa.H, (unsigned)((pa.N + 31) / 32), (unsigned)pa.B),
+                     dim3(64 * 3 * NBD), lds, stream, pa);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+// x -> MX codes along C (rows_prep), then the projection kernel writing the q / k
+// operands (rq, rk) and V's transposed codes (cv)
+static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, const AttnLayout& L,
+                           const RowsPrepArgs& rq, const RowsPrepArgs& rk, const ColsPrepArgs& cv, unsigned char* ws,
+                           hipStream_t stream) {
+  const int nbk = (xq.C + 31) / 32, Cpad = 32 * nbk;
+  const int64_t tokens = (int64_t)pp.B * pp.N;
+  RowsPrepArgs rx{};
+  rx.x = xq.x; rx.s0 = 0; rx.s1 = 0; rx.s2 = xq.x_row_stride;
+  rx.H = 1; rx.R = tokens; rx.rows = tokens; rx.D = xq.C; rx.nb = nbk; rx.dpad = Cpad;
+  rx.vec4 = aligned16(xq.x) && xq.x_row_stride % 4 == 0;
+  rx.op_kind = MXA_OP_MXINT8; rx.flush = pp.flush_subnormals; rx.bfloat = pp.bfloat;
+  rx.codes = reinterpret_cast<int8_t*>(ws + L.xc);
+  rx.sT = reinterpret_cast<int16_t*>(ws + L.xs);
+  int rc = launch_rows_prep(rx, stream);
+  if (rc) return rc;
+  ProjArgs pa{};
+  pa.xc = rx.codes; pa.xs = rx.sT;
+  const int out_f = 3 * pp.H * pp.D;
+  pa.wc = static_cast<const int8_t*>(xq.wq);
+  pa.ws = reinterpret_cast<const int16_t*>(static_cast<const unsigned char*>(xq.wq) + linear_exps_offset(out_f, xq.C));
+  pa.bias = xq.bias; pa.qkv_out = xq.qkv_out;
+  pa.B = pp.B; pa.N = pp.N; pa.H = pp.H; pa.D = pp.D; pa.nbk = nbk; pa.Cpad = Cpad; pa.bfloat = pp.bfloat;
+  pa.rq = rq; pa.rk = rk; pa.cv = cv;
+  switch ((pp.D + 31) / 32) {
+    case 1: return launch_proj_nbd<1>(pa, stream);
+    case 2: return launch_proj_nbd<2>(pa, stream);
+    case 3: return launch_proj_nbd<3>(pa, stream);
+    default: return launch_proj_nbd<4>(pa, stream);
+  }
+}
+
 // plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing;
 // scores_only: the approximate (or true) scores into p->pred_out / true_out, no top-k
+// xq: the fused qkv projection (q, k, v produced from x and the prepared weight)
 static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr,
-                          bool scores_only = false) {
-  if (!p || !p->q || !p->k) return MXA_ERR_ARG;
-  if (!scores_only && (!p->v || !p->out)) return MXA_ERR_ARG;
+                          bool scores_only = false, const mxa_qkv_params* xq = nullptr) {
+  if (!p) return MXA_ERR_ARG;
+  if (xq) {
+    if (!xq->x || !xq->wq || xq->C <= 0 || xq->x_row_stride < xq->C || p->N != p->T || scores_only) return MXA_ERR_ARG;
+  } else if (!p->q || !p->k) {
+    return MXA_ERR_ARG;
+  }
+  if (!scores_only && ((!p->v && !xq) || !p->out)) return MXA_ERR_ARG;
   if (scores_only && !(p->approx ? p->pred_out : p->true_out)) return MXA_ERR_ARG;
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
   if (!scores_only && p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
@@ -358,7 +423,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   const bool ranked = topk || scores_only;  // the selection kernel runs
   const int mode = score_mode(&pp, ranked);
   if (mode == kModeElsa && (!pp.elsa_proj || pp.N != pp.T)) return MXA_ERR_ARG;  // elsa_approximation.py:126, :142
-  const AttnLayout L = attn_layout(&pp, mode);
+  const AttnLayout L = attn_layout(&pp, mode, xq);
   const int64_t BH = (int64_t)pp.B * pp.H;
 
   int opq = MXA_OP_SIGN, opk = MXA_OP_SIGN;
@@ -403,8 +468,10 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   rq.signs = mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.qsg) : nullptr;
   rq.sA = need_sa ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
   if (ev) (void)hipEventRecord(ev[0], stream);
-  rc = launch_rows_prep(rq, stream);
-  if (rc) return rc;
+  if (!xq) {
+    rc = launch_rows_prep(rq, stream);
+    if (rc) return rc;
+  }
   if (ev) (void)hipEventRecord(ev[1], stream);
 
   RowsPrepArgs rk = rq;
@@ -418,7 +485,17 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   rk.zind = mode == kModeTrueEx ? reinterpret_cast<int8_t*>(ws + L.kz) : nullptr;
   rk.signs = mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.ksg) : nullptr;
   rk.sA = need_sa ? reinterpret_cast<int16_t*>(ws + L.ksA) : nullptr;
-  rc = launch_rows_prep(rk, stream);
+  ColsPrepArgs cv{};
+  cv.x = pp.v; cv.s0 = pp.v_strides[0]; cv.s1 = pp.v_strides[1]; cv.s2 = pp.v_strides[2];
+  cv.H = pp.H; cv.mats = BH; cv.R = pp.T; cv.C = pp.D; cv.nb = L.ntb; cv.rpad = L.tpad;
+  cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat;
+  cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
+  cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
+  if (xq) {
+    rc = launch_qkv_proj(pp, *xq, L, rq, rk, cv, ws, stream);
+  } else {
+    rc = launch_rows_prep(rk, stream);
+  }
   if (rc) return rc;
   if (mode == kModeElsa) {  // hashes of MX(Q), MX(K); norms of MX(K) rows
     ElsaPrepArgs eq{};
@@ -436,13 +513,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
 
-  if (!scores_only) {
-    ColsPrepArgs cv{};
-    cv.x = pp.v; cv.s0 = pp.v_strides[0]; cv.s1 = pp.v_strides[1]; cv.s2 = pp.v_strides[2];
-    cv.H = pp.H; cv.mats = BH; cv.R = pp.T; cv.C = pp.D; cv.nb = L.ntb; cv.rpad = L.tpad;
-    cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat;
-    cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
-    cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
+  if (!scores_only && !xq) {
     rc = launch_cols_prep(cv, stream);
     if (rc) return rc;
   }
@@ -483,6 +554,37 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   return MXA_OK;
 }
 
+extern "C" int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features) {
+  if (out_features <= 0 || in_features <= 0) return -1;
+  return linear_exps_offset(out_features, in_features) + align_up((int64_t)out_features * ((in_features + 31) / 32) * 2);
+}
+
+extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features,
+                                      int32_t flush_subnormals, int32_t bfloat, void* wq, hipStream_t stream) {
+  if (!w || !wq || out_features <= 0 || in_features <= 0) return MXA_ERR_ARG;
+  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
+  if (!aligned16(wq)) return MXA_ERR_ARG;
+  const int nbk = (in_features + 31) / 32;
+  RowsPrepArgs rw{};
+  rw.x = w; rw.s0 = 0; rw.s1 = 0; rw.s2 = in_features;
+  rw.H = 1; rw.R = out_features; rw.rows = out_features; rw.D = in_features; rw.nb = nbk; rw.dpad = 32 * nbk;
+  rw.vec4 = aligned16(w) && in_features % 4 == 0;
+  rw.op_kind = MXA_OP_MXINT8; rw.flush = flush_subnormals; rw.bfloat = bfloat;
+  rw.codes = static_cast<int8_t*>(wq);
+  rw.sT = reinterpret_cast<int16_t*>(static_cast<unsigned char*>(wq) + linear_exps_offset(out_features, in_features));
+  return launch_rows_prep(rw, stream);
+}
+
+extern "C" int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* xq) {
+  if (!p || !xq || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0 || xq->C <= 0) return -1;
+  return attn_layout(p, score_mode(p, p->top_k || p->pred_out), xq).total;
+}
+
+extern "C" int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream) {
+  if (!xq) return MXA_ERR_ARG;
+  return attention_impl(p, stream, nullptr, nullptr, false, xq);
+}
+
 extern "C" int mxa_approx_scores(const mxa_attn_params* p, hipStream_t stream) {
   return attention_impl(p, stream, nullptr, nullptr, true);
 }
@@ -497,13 +599,15 @@ extern "C" int mxa_attention_path(const mxa_attn_params* p) {
   return rc ? rc : plan;
 }
 
-extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms) {
+static int timed_impl(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream, int32_t iters,
+                      float* stage_ms) {
   if (iters <= 0 || !stage_ms) return MXA_ERR_ARG;
   std::vector<hipEvent_t> ev((size_t)iters * MXA_ATTN_STAGES_PLUS1);
   for (auto& e : ev)
     if (hipEventCreate(&e) != hipSuccess) return MXA_ERR_LAUNCH;
   int rc = MXA_OK;
-  for (int i = 0; i < iters && rc == MXA_OK; ++i) rc = attention_impl(p, stream, &ev[(size_t)i * MXA_ATTN_STAGES_PLUS1]);
+  for (int i = 0; i < iters && rc == MXA_OK; ++i)
+    rc = attention_impl(p, stream, &ev[(size_t)i * MXA_ATTN_STAGES_PLUS1], nullptr, false, xq);
   if (rc == MXA_OK && hipStreamSynchronize(stream) != hipSuccess) rc = MXA_ERR_LAUNCH;
   if (rc == MXA_OK) {
     for (int s = 0; s < MXA_ATTN_STAGES; ++s) {
@@ -518,6 +622,16 @@ extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream,
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
+}
+
+extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms) {
+  return timed_impl(p, nullptr, stream, iters, stage_ms);
+}
+
+extern "C" int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream,
+                                       int32_t iters, float* stage_ms) {
+  if (!xq) return MXA_ERR_ARG;
+  return timed_impl(p, xq, stream, iters, stage_ms);
 }
 
 // ---- standalone top-k: one DPP row per row (mxa_topk_grp.hpp) -----------------------

@@ -1,0 +1,162 @@
+// Per-block bodies of the attention operand builders, shared by the standalone
+// prep kernels (mxa_quant.hip) and the fused qkv projection (mxa_proj.hpp).
+#pragma once
+#include "mxa_kernels.hpp"
+
+namespace mxa {
+
+// ---------------------------------------------------------------------------
+// attention operand builder for rows quantized along the last axis (Q, K)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int exion_m(int raw) {
+  // two_step_leading_ones on an integer code (funcs/exponent_based_prediction.py:110-127):
+  //   l1 = floor(log2|raw|), t = max(raw - 2^l1, 0) (signed!), l2 = floor(log2 t),
+  //   approx = sign(raw) * e * (2^l1 + 2^l2) / 64   (2^-126 terms vanish in fp32)
+  if (raw == 0) return 0;
+  if (raw < 0) return -(1 << (31 - __clz(-raw)));
+  const int p1 = 1 << (31 - __clz(raw));
+  const int t = raw - p1;
+  return p1 + (t > 0 ? (1 << (31 - __clz(t))) : 0);
+}
+
+// One 32-element block of a row, 8 lanes x 4 elements (lane sub = 0..7 of an
+// 8-lane group, c0 = 32 blk + 4 sub): MXINT8 codes, block exponent, approximator
+// operand and sign word into the RowsPrepArgs outputs (row `row`, block `blk`).
+// The 8 lanes of a group must be consecutive and all call it (DPP reductions).
+__device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t row, int blk, int sub, int c0,
+                                                float xv[4], bool valid) {
+  uint32_t mb = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    xv[j] = round_bfloat(xv[j], a.bfloat, kRoundNearest, 1);
+    const uint32_t ub = __float_as_uint(xv[j]) & 0x7FFFFFFFu;
+    mb = ub > mb ? ub : mb;
+  }
+  mb = oct_reduce(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  int e_raw;
+  const int es = scale_exponent(mb, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  if (a.flush && !(e_raw != kExpNaN && e_raw > -127)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = xv[j] * 0.0f;
+  }
+  int code[4];
+  int maxc = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    code[j] = nanblk ? 0 : (int)round_code(xv[j], es, 8, kRoundNearest);
+    const int ac = code[j] < 0 ? -code[j] : code[j];
+    maxc = ac > maxc ? ac : maxc;
+  }
+  maxc = (int)oct_reduce((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
+  // floor(log2(max |MX|)), unclamped; MX max = maxc * 2^(es-6) exactly.
+  int eA;
+  if (nanblk) eA = kExpNaN;
+  else if (maxc == 0) eA = -126;
+  else eA = floor_log2_pos((float)maxc * pow2f(es - 6));
+  int op[4];
+  int sA;
+  switch (a.op_kind) {
+    case MXA_OP_SIGN:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = (c0 + j < a.D) ? (code[j] < 0 ? -1 : 1) : 0;
+      sA = eA;
+      break;
+    case MXA_OP_MXINT4:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest);
+      sA = nanblk ? kExpNaN : es - 2;
+      break;
+    case MXA_OP_EXION: {
+      const int sh = nanblk ? 0 : es - eA;  // MX / 2^eA * 64 = code * 2^(es-eA), an integer < 128
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : exion_m(code[j] << sh);
+      sA = eA;
+      break;
+    }
+    case MXA_OP_TRUE_EX:
+      // exponent_based_sign_leading_ones (examples/deit/exponent_based_prediction.py:163-178):
+      // (mx < 0 ? -1 : 1) * 2^floor(log2|mx|), zeros -> +1.  Nonzero elements as the
+      // power-of-two code sign * 2^floor(log2|code|) in units of 2^(es-6); zeros in zind
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ac = code[j] < 0 ? -code[j] : code[j];
+        const int p2 = ac ? 1 << (31 - __clz(ac)) : 0;
+        op[j] = code[j] < 0 ? -p2 : p2;
+      }
+      // a NaN block's MX values are NaN, and get_true_exponents maps them like zeros
+      // (mask |x| > 0 is false: exponent 0, value +1; examples :98-110): codes 0, zind 1
+      sA = nanblk ? 0 : es - 6;
+      break;
+    default:  // MXA_OP_MXINT8
+#pragma unroll
+      for (int j = 0; j < 4; ++j) op[j] = code[j];
+      sA = nanblk ? kExpNaN : es - 6;
+      break;
+  }
+  if (valid) {
+    const int64_t base = row * a.dpad + c0;
+    const uint32_t pc = (uint32_t)(code[0] & 0xFF) | ((uint32_t)(code[1] & 0xFF) << 8) |
+                        ((uint32_t)(code[2] & 0xFF) << 16) | ((uint32_t)(code[3] & 0xFF) << 24);
+    const uint32_t po = (uint32_t)(op[0] & 0xFF) | ((uint32_t)(op[1] & 0xFF) << 8) |
+                        ((uint32_t)(op[2] & 0xFF) << 16) | ((uint32_t)(op[3] & 0xFF) << 24);
+    if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
+    if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
+    if (a.zind) {
+      uint32_t pz = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pz |= (c0 + j < a.D && code[j] == 0 ? 1u : 0u) << (8 * j);
+      *reinterpret_cast<uint32_t*>(a.zind + base) = pz;
+    }
+  }
+  // packed sign word of the block, bit (4*sub + j) = (code < 0): the exp-sign
+  // operand of ex_pred (codes beyond D are 0, i.e. positive)
+  uint32_t sw = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sw |= (code[j] < 0 ? 1u : 0u) << (4 * sub + j);
+  sw = oct_reduce(sw, [](uint32_t u, uint32_t w) { return u | w; });
+  if (valid && sub == 0) {
+    if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
+    if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
+    if (a.signs) a.signs[row * a.nb + blk] = sw;
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// operand builder for matrices quantized along the row axis (V, and in2 of
+// mx.matmul): blocks of 32 rows per column; output transposed [col][row] codes.
+// ---------------------------------------------------------------------------
+// One 32-row block of one column (m = matrix, blk, column c) from its 32 values
+// (already bfloat-rounded, zero beyond the matrix): codes into the transposed
+// [m][C][rpad] table, the exponent into [m][nb][C].
+__device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t m, int blk, int c, const float xv[32],
+                                                 uint32_t mx) {
+  const int r0 = blk * 32;
+  int e_raw;
+  const int es = scale_exponent(mx, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  uint32_t w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = xv[q * 4 + j];
+      if (flush) v = v * 0.0f;
+      const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest);
+      acc |= (uint32_t)(cd & 0xFF) << (8 * j);
+    }
+    w[q] = acc;
+  }
+  int8_t* dst = a.codes_t + (m * a.C + c) * a.rpad + r0;
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  a.scale[(m * a.nb + blk) * a.C + c] = exp_to16(nanblk ? kExpNaN : es - (a.mbits - 2));
+}
+
+
+}  // namespace mxa

@@ -296,6 +296,72 @@ def mx_approx_scores(q: torch.Tensor, k: torch.Tensor, pred_mode: str = "ex_pred
     return pred
 
 
+class LinearWeightMX:
+    """A Linear weight (out_features, in_features) as MXINT8 codes + block exponents
+    along in_features on the device (mxa_linear_weight_prep): prepared once, reused by
+    every fused call (the weights are constant at inference)."""
+
+    def __init__(self, weight: torch.Tensor, flush_subnormals: bool = False, bfloat: int = 0):
+        dev = require_device(weight)
+        w = _f32(weight.detach(), "weight").contiguous()
+        self.out_features, self.in_features = w.shape
+        nbytes = lib().mxa_linear_weight_bytes(self.out_features, self.in_features)
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        check(lib().mxa_linear_weight_prep(w.data_ptr(), self.out_features, self.in_features, int(bool(flush_subnormals)),
+                                           int(bfloat), self.buf.data_ptr(), stream_ptr(dev)), "mxa_linear_weight_prep")
+        self.flush, self.bfloat = bool(flush_subnormals), int(bfloat)
+
+
+def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_heads: int, scale: float,
+                     k_top: int = 20, pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
+                     flush_subnormals: bool = False, bfloat: int = 0, return_qkv: bool = False,
+                     elsa_proj: Optional[torch.Tensor] = None):
+    """The qkv mx.Linear fused into the attention core (include/mxa.h mxa_qkv_attention):
+    x (B, N, C) float32 tokens; weight a (3C', C) tensor or a LinearWeightMX; returns
+    (out (B,H,N,D), idx (B,H,N,k) or None[, qkv (B,N,3C') fp32 projection])."""
+    dev = require_device(x, bias, elsa_proj)
+    x = _f32(x, "x")
+    if x.dim() != 3 or x.stride(2) != 1:
+        raise ValueError("x must be (B, N, C) with contiguous C")
+    B, Ntok, C = x.shape
+    wq = weight if isinstance(weight, LinearWeightMX) else LinearWeightMX(weight, flush_subnormals, bfloat)
+    if wq.in_features != C or wq.out_features % (3 * num_heads):
+        raise ValueError(f"weight ({wq.out_features}, {wq.in_features}) does not fit x C={C}, heads={num_heads}")
+    if (wq.flush, wq.bfloat) != (bool(flush_subnormals), int(bfloat)):
+        raise ValueError("the prepared weight was quantized with other flush / bfloat settings")
+    D = wq.out_features // (3 * num_heads)
+    if top_k and not (0 < k_top <= Ntok):
+        raise ValueError(f"k={k_top} out of range for {Ntok} keys")
+    if approx and top_k and pred_mode not in N.PRED_MODES:
+        raise ValueError(f"pred_mode {pred_mode!r} not supported")
+    # q / k / v are produced inside the call: stand-in views carry the shapes only
+    shape_q = torch.empty((D,), device=dev).as_strided((B, num_heads, Ntok, D), (0, 0, 0, 1))
+    p, _, _, keep = _attn_params(shape_q, shape_q, shape_q, scale, k_top, pred_mode, top_k, approx and top_k, None,
+                                 flush_subnormals, bfloat, elsa_proj)
+    p.q = p.k = p.v = None
+    out = torch.empty((B, num_heads, Ntok, D), dtype=torch.float32, device=dev)
+    p.out = out.data_ptr()
+    p.out_strides[:] = (out.stride(0), out.stride(1), out.stride(2))
+    idx = torch.empty((B, num_heads, Ntok, k_top), dtype=torch.int64, device=dev) if top_k else None
+    p.idx_out = idx.data_ptr() if idx is not None else None
+    xp = N.QkvParams()
+    xp.x, xp.x_row_stride, xp.C, xp.wq = x.data_ptr(), x.stride(1), C, wq.buf.data_ptr()
+    if B > 1 and x.stride(0) != Ntok * x.stride(1):
+        raise ValueError("x rows must be evenly strided over (B, N)")
+    if bias is not None:
+        bias = _f32(bias, "bias").contiguous()
+        xp.bias = bias.data_ptr()
+    qkv = torch.empty((B, Ntok, wq.out_features), dtype=torch.float32, device=dev) if return_qkv else None
+    xp.qkv_out = qkv.data_ptr() if return_qkv else None
+    nbytes = lib().mxa_qkv_attention_workspace_bytes(ctypes.byref(p), ctypes.byref(xp))
+    if nbytes < 0:
+        raise ValueError("bad shape")
+    ws = _workspace(dev, nbytes)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    check(lib().mxa_qkv_attention(ctypes.byref(p), ctypes.byref(xp), stream_ptr(dev)), "mxa_qkv_attention")
+    return (out, idx, qkv) if return_qkv else (out, idx)
+
+
 def selftest_mfma(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     dev = require_device(a, b)
     c = torch.empty((16, 16), dtype=torch.int32, device=dev)

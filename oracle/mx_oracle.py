@@ -310,6 +310,25 @@ def mx_matmul(A, B, elem="int8", block_size=32, flush=False, bfloat=32):
     return quantize_bfloat(exact_matmul_f32(qa, qb), bfloat)
 
 
+def mx_linear(x, W, bias=None, elem="int8", block_size=32, flush=False, bfloat=32):
+    """mx.Linear forward (microxscaling/mx/linear.py:20-103): bf(fl32(MX(bf(x)) @ MX(bf(W))^T)),
+    then bf(out + bf(bias)); both operands MX-quantized along in_features.
+    Exact-then-round (the reference's fp32 GEMM order is unpinned: equal within rounding)."""
+    qx = quantize_mx(quantize_bfloat(x, bfloat), elem, block_size, -1, flush=flush)[0]
+    qw = quantize_mx(quantize_bfloat(W, bfloat), elem, block_size, -1, flush=flush)[0]
+    out = quantize_bfloat(exact_matmul_f32(qx, np.swapaxes(qw, -1, -2)), bfloat)
+    if bias is not None:
+        out = quantize_bfloat((out + quantize_bfloat(np.asarray(bias, F32), bfloat)).astype(F32), bfloat)
+    return out
+
+
+def qkv_split(qkv, H):
+    """qkv.reshape(B, N, 3, H, D).permute(2, 0, 3, 1, 4) (deit main.py:87-88, DiT models.py:156-157)."""
+    B, N, C3 = qkv.shape
+    t = qkv.reshape(B, N, 3, H, C3 // (3 * H)).transpose(2, 0, 3, 1, 4)
+    return t[0], t[1], t[2]
+
+
 # ---------------------------------------------------------------------------
 # top-k (oracle/topk_ref.cpp)
 # ---------------------------------------------------------------------------

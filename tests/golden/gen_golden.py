@@ -209,6 +209,28 @@ def gen_attention_extra():
     print("wrote attn_extra")
 
 
+def gen_linear_qkv():
+    """linear_qkv.npz: the reference's mx.Linear qkv projection (linear.py:20-103) at the
+    DeiT-tiny block shape (C = 192, 3 heads of 64; deit main.py:59-64, :87-88), then its
+    ex_pred top-k attention on the reference's own q, k, v."""
+    from mx import Linear
+    x = torch.from_numpy(rnd((1, 197, 192), 30))
+    W = torch.from_numpy(rnd((576, 192), 31, 0.08))
+    bias = torch.from_numpy(rnd((576,), 32, 0.1))
+    lin = Linear(192, 576, bias=True, mx_specs=specs())
+    lin.weight.data = W.clone()
+    lin.bias.data = bias.clone()
+    with torch.no_grad():
+        qkv = lin(x)
+    q, k, v = qkv.reshape(1, 197, 3, 3, 64).permute(2, 0, 3, 1, 4)
+    sc = 64 ** -0.5
+    r = attention_glue(q.contiguous(), k.contiguous(), v.contiguous(), specs(), sc, 20, "ex_pred")
+    np.savez_compressed(os.path.join(OUT, "linear_qkv.npz"), x=x.numpy(), W=W.numpy(), bias=bias.numpy(),
+                        qkv=qkv.numpy(), scale=np.float32(sc), pred=r["pred"], idx=r["idx"], out=r["out"],
+                        true=r["true"])
+    print("wrote linear_qkv")
+
+
 def gen_quant_kat():
     """Known-answer + boundary vectors through the reference's _quantize_mx."""
     out = {}
@@ -330,6 +352,6 @@ def gen_topk_ties():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra"]
+    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv"]
     for w in which:
         globals()["gen_" + w]()

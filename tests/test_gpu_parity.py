@@ -488,3 +488,56 @@ def test_linear_dropin(M):
     y = lin(x)
     want = O.mx_matmul(host(x), host(lin.weight).T) + host(lin.bias)
     assert np.max(np.abs(host(y) - want)) <= 1e-5 * max(1.0, np.abs(want).max())
+
+
+# ------------------------------------------------------------------ fused qkv projection
+def test_qkv_attention_vs_reference(M):
+    """mx.Linear qkv projection fused into operand production (mxa_qkv_attention) against
+    the reference's Linear + attention chain (linear_qkv.npz)."""
+    d = load("linear_qkv.npz")
+    out, idx, qkv = M.mx_qkv_attention(dev(d["x"]), dev(d["W"]), dev(d["bias"]), 3, float(d["scale"]), k_top=20,
+                                       return_qkv=True)
+    torch.cuda.synchronize()
+    same(host(qkv), d["qkv"], "qkv projection")
+    same(host(idx), d["idx"], "idx")
+    assert O.normwise_rel_err(host(out), d["out"]) <= OUT_TOL
+
+
+@pytest.mark.parametrize("mode", ["ex_pred", "MXINT4", "two_step_leading_ones", "true_ex", "partial_Q", "ELSA"])
+@pytest.mark.parametrize("B,N,C,H", [(2, 197, 768, 12), (1, 256, 1152, 16), (3, 45, 96, 2)])
+def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
+    """The fused projection + attention against the oracle chained the same way (exact
+    projection, split, attention) at the DeiT-base and DiT-XL/2 block widths and a
+    ragged small case; NaN token row and zero weight row included."""
+    D = C // H
+    if mode == "ELSA" and D not in (64, 72):
+        pytest.skip("ELSA's structured matrix exists for d = 64, 72 only")
+    rng = np.random.default_rng(B * 1000 + N)
+    x = rng.standard_normal((B, N, C), dtype=np.float32)
+    W = (rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(0.05)).astype(np.float32)
+    bias = (rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+    x[0, 3, 7] = np.nan
+    W[5] = 0.0
+    k = min(20, N)
+    proj = None
+    if mode == "ELSA":
+        from mx_quantization_amd.funcs import _create_structured_orthogonal_matrix
+        torch.manual_seed(D)
+        proj = _create_structured_orthogonal_matrix(D).numpy()
+    wq = M.LinearWeightMX(dev(W))
+    out, idx, qkv = M.mx_qkv_attention(dev(x), wq, dev(bias), H, D ** -0.5, k_top=k, pred_mode=mode,
+                                       return_qkv=True, elsa_proj=None if proj is None else dev(proj))
+    torch.cuda.synchronize()
+    want_qkv = O.mx_linear(x, W, bias)
+    same(host(qkv), want_qkv, "qkv")
+    # the operands the fused kernel produced equal those of the unfused op on its q, k, v
+    q, kk, v = O.qkv_split(want_qkv, H)
+    sub = slice(0, 1)  # oracle on the first image (all images through the unfused op)
+    r = O.attention(q[sub], kk[sub], v[sub], D ** -0.5, k_top=k, pred_mode=mode, elsa_proj=proj)
+    same(host(idx)[sub], r["idx"], "idx vs oracle")
+    o_fin = ~np.isnan(r["out"]).any(-1)
+    assert O.normwise_rel_err(host(out)[sub][o_fin], r["out"][o_fin]) <= OUT_TOL
+    o2, i2 = M.mx_topk_attention(*(dev(np.ascontiguousarray(t)) for t in (q, kk, v)), D ** -0.5, k_top=k,
+                                 pred_mode=mode, elsa_proj=None if proj is None else dev(proj))
+    same(host(idx), host(i2), "idx vs unfused op")
+    same(host(out), host(o2), "out vs unfused op")

@@ -215,3 +215,17 @@ def test_dropin_structured_orthogonal_matrix(d):
     torch.manual_seed(int(ex[f"{tag}/proj_seed"]))
     P = _create_structured_orthogonal_matrix(d).numpy()
     same(P, ex[f"{tag}/proj"])
+
+
+def test_linear_qkv_chain_vs_reference():
+    """The oracle's mx.Linear (exact-then-round) on the reference's qkv fixture, and the
+    ex_pred attention chained on it (linear_qkv.npz from gen_golden.py)."""
+    d = load("linear_qkv.npz")
+    qkv = O.mx_linear(d["x"], d["W"], d["bias"])
+    same(qkv, d["qkv"])
+    q, k, v = O.qkv_split(qkv, 3)
+    r = O.attention(q, k, v, float(d["scale"]), k_top=20)
+    same(r["true"], d["true"])
+    same(r["pred"], d["pred"])
+    same(r["idx"], d["idx"])
+    assert O.normwise_rel_err(r["out"], d["out"]) <= 1e-3
