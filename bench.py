@@ -307,7 +307,7 @@ def run_qkv(c, images, steps, warmup, device, world):
     x = torch.from_numpy(rng.standard_normal((B, Nt, C), dtype=np.float32)).to(device)
     W = torch.from_numpy((rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(C ** -0.5))).to(device)
     bias = torch.from_numpy(rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.02)).to(device)
-    wq = M.LinearWeightMX(W)
+    wq = M.LinearWeightMX(W, D)
     for _ in range(max(warmup, 1)):
         M.mx_qkv_attention(x, wq, bias, H, c["scale"], k_top=c["k"], pred_mode=c["mode"])
     torch.cuda.synchronize()

@@ -203,7 +203,8 @@ int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t it
  *
  * mxa_linear_weight_prep: W (out_features, in_features) fp32 row-major -> MXINT8 codes +
  * block exponents along in_features into `wq` (mxa_linear_weight_bytes bytes, 16-B
- * aligned; once per weight).  out_features = 3 * H * D for the qkv projection.
+ * aligned; once per weight), laid out MFMA-ready in column groups of group_width
+ * (the qkv projection: out_features = 3 * H * D, group_width = D -- one head's q, k or v).
  *
  * mxa_qkv_attention: mxa_attention with q, k, v produced from x (p->q, p->k, p->v are
  * ignored; self-attention, p->N == p->T).  The projection is exact-then-rounded (the
@@ -213,14 +214,14 @@ typedef struct mxa_qkv_params {
   const float* x;        /* (B*N, C) tokens, row stride x_row_stride (elements)            */
   int64_t x_row_stride;
   int32_t C;             /* in_features                                                     */
-  const void* wq;        /* mxa_linear_weight_prep output for W (3*H*D, C)                  */
+  const void* wq;        /* mxa_linear_weight_prep output for W (3*H*D, C), group_width D    */
   const float* bias;     /* (3*H*D) or null                                                 */
   float* qkv_out;        /* optional (B*N, 3*H*D) fp32 projection (tests)                   */
 } mxa_qkv_params;
 
-int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features);
-int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features, int32_t flush_subnormals,
-                           int32_t bfloat, void* wq, hipStream_t stream);
+int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features, int32_t group_width);
+int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features, int32_t group_width,
+                           int32_t flush_subnormals, int32_t bfloat, void* wq, hipStream_t stream);
 int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* x);
 int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream);
 /* mxa_attention_timed for the fused projection path (stage 1 = x quantize + projection) */

@@ -64,8 +64,8 @@ _SIGS = {
     "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_attention_path": (c_i32, [ctypes.POINTER(AttnParams)]),
     "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
-    "mxa_linear_weight_bytes": (c_i64, [c_i32, c_i32]),
-    "mxa_linear_weight_prep": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "mxa_linear_weight_bytes": (c_i64, [c_i32, c_i32, c_i32]),
+    "mxa_linear_weight_prep": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "mxa_qkv_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams)]),
     "mxa_qkv_attention": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp]),
     "mxa_qkv_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp, c_i32,

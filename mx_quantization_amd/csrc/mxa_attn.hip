@@ -344,12 +344,6 @@ static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, in
 }
 
 // ---- fused qkv projection (mxa_proj.hpp) ------------------------------------------
-namespace {
-int64_t linear_exps_offset(int32_t out_features, int32_t in_features) {
-  return align_up((int64_t)out_features * ((in_features + 31) / 32) * 32);
-}
-}  // namespace
-
 template <int NBD>
 static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   const size_t lds = proj_lds(pa.Cpad, pa.nbk, pa.D).total;
@@ -357,8 +351,8 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)pa.H, (unsigned)((pa.N + 31) / 32), (unsigned)pa.B),
-                     dim3(64 * 3 * NBD), lds, stream, pa);
+  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B), dim3(64 * 3 * NBD), lds,
+                     stream, pa);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
@@ -378,13 +372,18 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   rx.sT = reinterpret_cast<int16_t*>(ws + L.xs);
   int rc = launch_rows_prep(rx, stream);
   if (rc) return rc;
+  const LinearLayout W = linear_layout(3 * pp.H * pp.D, xq.C, pp.D);
+  const unsigned char* wb = static_cast<const unsigned char*>(xq.wq);
   ProjArgs pa{};
   pa.xc = rx.codes; pa.xs = rx.sT;
-  const int out_f = 3 * pp.H * pp.D;
-  pa.wc = static_cast<const int8_t*>(xq.wq);
-  pa.ws = reinterpret_cast<const int16_t*>(static_cast<const unsigned char*>(xq.wq) + linear_exps_offset(out_f, xq.C));
+  pa.pk = reinterpret_cast<const int8_t*>(wb + W.pk);
+  pa.pe = reinterpret_cast<const int16_t*>(wb + W.pe);
+  pa.ps = reinterpret_cast<const int16_t*>(wb + W.ps);
   pa.bias = xq.bias; pa.qkv_out = xq.qkv_out;
   pa.B = pp.B; pa.N = pp.N; pa.H = pp.H; pa.D = pp.D; pa.nbk = nbk; pa.Cpad = Cpad; pa.bfloat = pp.bfloat;
+  // shifted int32 block sums stay exact while nbk * 32 * 127^2 * 2^smax < 2^31
+  pa.smax = -1;
+  while ((int64_t)nbk * 516128 * ((int64_t)1 << (pa.smax + 1)) < ((int64_t)1 << 31)) ++pa.smax;
   pa.rq = rq; pa.rk = rk; pa.cv = cv;
   switch ((pp.D + 31) / 32) {
     case 1: return launch_proj_nbd<1>(pa, stream);
@@ -554,25 +553,36 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   return MXA_OK;
 }
 
-extern "C" int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features) {
-  if (out_features <= 0 || in_features <= 0) return -1;
-  return linear_exps_offset(out_features, in_features) + align_up((int64_t)out_features * ((in_features + 31) / 32) * 2);
+extern "C" int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features, int32_t group_width) {
+  if (out_features <= 0 || in_features <= 0 || group_width <= 0 || out_features % group_width) return -1;
+  return linear_layout(out_features, in_features, group_width).total;
 }
 
-extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features,
+extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features, int32_t group_width,
                                       int32_t flush_subnormals, int32_t bfloat, void* wq, hipStream_t stream) {
-  if (!w || !wq || out_features <= 0 || in_features <= 0) return MXA_ERR_ARG;
+  if (!w || !wq || out_features <= 0 || in_features <= 0 || group_width <= 0 || out_features % group_width)
+    return MXA_ERR_ARG;
   if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
   if (!aligned16(wq)) return MXA_ERR_ARG;
-  const int nbk = (in_features + 31) / 32;
+  const LinearLayout W = linear_layout(out_features, in_features, group_width);
+  unsigned char* wb = static_cast<unsigned char*>(wq);
   RowsPrepArgs rw{};
   rw.x = w; rw.s0 = 0; rw.s1 = 0; rw.s2 = in_features;
-  rw.H = 1; rw.R = out_features; rw.rows = out_features; rw.D = in_features; rw.nb = nbk; rw.dpad = 32 * nbk;
+  rw.H = 1; rw.R = out_features; rw.rows = out_features; rw.D = in_features; rw.nb = W.nbk; rw.dpad = W.Cpad;
   rw.vec4 = aligned16(w) && in_features % 4 == 0;
   rw.op_kind = MXA_OP_MXINT8; rw.flush = flush_subnormals; rw.bfloat = bfloat;
-  rw.codes = static_cast<int8_t*>(wq);
-  rw.sT = reinterpret_cast<int16_t*>(static_cast<unsigned char*>(wq) + linear_exps_offset(out_features, in_features));
-  return launch_rows_prep(rw, stream);
+  rw.codes = reinterpret_cast<int8_t*>(wb + W.rawc);
+  rw.sT = reinterpret_cast<int16_t*>(wb + W.rawe);
+  int rc = launch_rows_prep(rw, stream);
+  if (rc) return rc;
+  const int64_t pcols = (int64_t)W.G * W.NB32 * 32;
+  hipLaunchKernelGGL(linear_pack_kernel, dim3((unsigned)((pcols * W.nbk + 255) / 256)), dim3(256), 0, stream,
+                     rw.codes, rw.sT, out_features, group_width, W.NB32, W.nbk, W.Cpad, pcols,
+                     reinterpret_cast<int8_t*>(wb + W.pk), reinterpret_cast<int16_t*>(wb + W.pe));
+  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL(linear_stats_kernel, dim3((unsigned)((pcols + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps));
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
 extern "C" int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* xq) {

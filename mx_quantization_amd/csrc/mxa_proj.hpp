@@ -5,39 +5,125 @@
 // the Linear forward is microxscaling/mx/linear.py:20-103:
 //   out = bf(fl32(MX(bf(x), along C) @ MX(bf(W), along C)^T));  out = bf(out + bf(bias))
 // (bf = quantize_elemwise_op, identity at bfloat 0/32).  Here one workgroup takes one
-// 32-token MX block of one image and one head: the x code tile (staged in LDS once)
-// times the head's q / k / v weight rows on v_mfma_i32_32x32x32_i8 -- K = 32 = one
+// 32-token MX block of one image: the x code tile (staged in LDS once) times each
+// head's q / k / v weight rows (prepared MFMA-ready: one coalesced load per K-block) on v_mfma_i32_32x32x32_i8 -- K = 32 = one
 // MX block, so each block's int32 sum is exact -- with the block scale 2^(ex + ew)
-// applied in fp64 (ldexp) and summed exactly, so the projection is the correctly
-// rounded exact product (the reference's MKL sgemm order is unpinned, SURVEY.md F7:
+// applied exactly -- as int32 sums shifted to the row's and column's smallest block
+// exponent (the common case; v_lshl_add_u32), else in fp64 -- so the projection is
+// the correctly rounded exact product (the reference's MKL sgemm order is unpinned, SURVEY.md F7:
 // tolerance there, bit-exact against the oracle).  The fp32 tile then stays in LDS
 // and is quantized in place into exactly what rows_prep / cols_prep would produce
 // from q, k, v: q and k rows (codes, block exponents, approximator operands) and V's
 // codes along the 32 tokens (transposed) -- the fp32 q / k / v never reach HBM.
 #pragma once
+#include <type_traits>
+
 #include "mxa_finish.hpp"
 #include "mxa_prep.hpp"
 
 namespace mxa {
 
+// Prepared Linear weight (mxa_linear_weight_prep): output columns in groups of gw (a
+// head's q, k or v: gw = D), each group padded to NB32 = ceil(gw/32) 32-column blocks.
+//   pk  MFMA-ready codes [group][cb][kb][lane 0..63][16 B]: lane = n + 32 h holds
+//       W[col n][32 kb + 16 h .. + 16] -- one coalesced 1-KB load per wave and K-block
+//   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
+//   ps  per padded column: smallest finite block exponent, spread (int16 pair)
+//   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
+struct LinearLayout {
+  int G, NB32, nbk, Cpad;
+  int64_t pk, pe, ps, rawc, rawe, total;
+};
+__host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int gw) {
+  LinearLayout L;
+  auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+  L.G = out_f / gw;
+  L.NB32 = (gw + 31) / 32;
+  L.nbk = (in_f + 31) / 32;
+  L.Cpad = 32 * L.nbk;
+  const int64_t pcols = (int64_t)L.G * L.NB32 * 32;
+  int64_t o = 0;
+  L.pk = o;
+  o += al(pcols * L.Cpad);
+  L.pe = o;
+  o += al(pcols * L.nbk * 2);
+  L.ps = o;
+  o += al(pcols * 4);
+  L.rawc = o;
+  o += al((int64_t)out_f * L.Cpad);
+  L.rawe = o;
+  o += al((int64_t)out_f * L.nbk * 2);
+  L.total = o;
+  return L;
+}
+
+// one thread per (padded column, K-block): the MFMA-ready codes and the exponents
+__global__ __launch_bounds__(256) void linear_pack_kernel(const int8_t* rawc, const int16_t* rawe, int out_f, int gw,
+                                                          int NB32, int nbk, int Cpad, int64_t pcols, int8_t* pk,
+                                                          int16_t* pe) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= pcols * nbk) return;
+  const int64_t pc = t / nbk;
+  const int kb = (int)(t - pc * nbk);
+  const int64_t blkc = pc / 32;  // group * NB32 + cb
+  const int n = (int)(pc - blkc * 32);
+  const int64_t g = blkc / NB32;
+  const int cb = (int)(blkc - g * NB32);
+  const int gc = 32 * cb + n;
+  const bool real = gc < gw;
+  const int64_t col = g * gw + gc;
+  uint4 lo = make_uint4(0, 0, 0, 0), hi = make_uint4(0, 0, 0, 0);
+  int16_t e = 0;
+  if (real) {
+    lo = *reinterpret_cast<const uint4*>(rawc + col * Cpad + 32 * kb);
+    hi = *reinterpret_cast<const uint4*>(rawc + col * Cpad + 32 * kb + 16);
+    e = rawe[col * nbk + kb];
+  }
+  int8_t* dst = pk + ((blkc * nbk + kb) * 64) * 16;
+  *reinterpret_cast<uint4*>(dst + n * 16) = lo;
+  *reinterpret_cast<uint4*>(dst + (n + 32) * 16) = hi;
+  pe[pc * nbk + kb] = e;
+}
+
+// per padded column: smallest finite block exponent and the spread
+__global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, int64_t pcols, int nbk, int16_t* ps) {
+  const int64_t pc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pc >= pcols) return;
+  int lo = 1 << 20, hi = -(1 << 20);
+  for (int kb = 0; kb < nbk; ++kb) {
+    const int e = exp_from16(pe[pc * nbk + kb]);
+    if (e != kExpNaN) {
+      lo = min(lo, e);
+      hi = max(hi, e);
+    }
+  }
+  if (lo > hi) lo = hi = 0;
+  ps[2 * pc] = (int16_t)lo;
+  ps[2 * pc + 1] = (int16_t)(hi - lo);
+}
+
 struct ProjArgs {
   const int8_t* xc;   // x codes [B*N][Cpad]
   const int16_t* xs;  // x code-unit exponents [B*N][nbk]
-  const int8_t* wc;   // W codes [3*H*D][Cpad]
-  const int16_t* ws;  // W code-unit exponents [3*H*D][nbk]
+  const int8_t* pk;   // prepared weight (LinearLayout with gw = D)
+  const int16_t* pe;
+  const int16_t* ps;
   const float* bias;  // [3*H*D] or null
   float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
   int B, N, H, D, nbk, Cpad, bfloat;
+  int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
   RowsPrepArgs rq, rk;  // q / k row outputs (rows_prep layout)
   ColsPrepArgs cv;      // V outputs (cols_prep layout)
 };
 
 struct ProjLds {
-  size_t xt, xe, rn, ot, total;
+  size_t xt, xe, rlo, rhi, rn, st, ot, total;
   int xst, ost;
 };
-// x code tile [32][Cpad + 16], x exponents [nbk][32] (int16, NaN -> 0), row NaN flags,
-// the fp32 output tile [32][3D + 1] (odd stride: V's column reads are conflict-free)
+// x code tile [32][Cpad + 16], x exponents relative to the row's smallest [nbk][32]
+// (int16, NaN -> 0), per-row smallest / largest exponent and NaN flag, tile stats, the
+// fp32 output tile of one head [32][3D + 1] (odd stride: V's column reads are
+// conflict-free)
 __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   ProjLds L;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -47,8 +133,14 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   o += (size_t)32 * L.xst;
   L.xe = o;
   o += al((size_t)nbk * 32 * 2);
+  L.rlo = o;
+  o += 32 * 4;
+  L.rhi = o;
+  o += 32 * 4;
   L.rn = o;
   o += 32 * 4;
+  L.st = o;
+  o += 16;
   L.ost = 3 * D + 1;
   L.ot = o;
   o += al((size_t)32 * L.ost * 4);
@@ -56,19 +148,25 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   return L;
 }
 
-// NBD: 32-blocks per head dim; 3 * NBD waves, wave (s, cb) = sub-matrix s (q, k, v)
-// and its 32-column block cb
+// One workgroup per (32-token block, image), looping over the heads; 3 * NBD waves,
+// wave (s, cb) = sub-matrix s (q, k, v) and its 32-column block cb of the head.
+#ifndef MXA_PROJ_WAVES
+#define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
+#endif
 template <int NBD>
-__global__ __launch_bounds__(64 * 3 * NBD) void qkv_proj_kernel(ProjArgs a) {
+__global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int kThreads = 64 * 3 * NBD;
-  const int h = blockIdx.x, tb = blockIdx.y, b = blockIdx.z;
+  const int tb = blockIdx.x, b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int D = a.D, HD = a.H * D;
-  const ProjLds L = proj_lds(a.Cpad, a.nbk, D);
+  const int D = a.D, HD = a.H * D, nbk = a.nbk;
+  const ProjLds L = proj_lds(a.Cpad, nbk, D);
   int8_t* xt = reinterpret_cast<int8_t*>(smem + L.xt);
   int16_t* xe = reinterpret_cast<int16_t*>(smem + L.xe);
+  int* rlo = reinterpret_cast<int*>(smem + L.rlo);
+  int* rhi = reinterpret_cast<int*>(smem + L.rhi);
   int* rn = reinterpret_cast<int*>(smem + L.rn);
+  int* st = reinterpret_cast<int*>(smem + L.st);
   float* ot = reinterpret_cast<float*>(smem + L.ot);
   const int n0 = 32 * tb, rows = min(32, a.N - n0);
   const int64_t row0 = (int64_t)b * a.N + n0;
@@ -81,20 +179,43 @@ __global__ __launch_bounds__(64 * 3 * NBD) void qkv_proj_kernel(ProjArgs a) {
     if (m < rows) v = *reinterpret_cast<const uint4*>(a.xc + (row0 + m) * a.Cpad + 16 * c);
     *reinterpret_cast<uint4*>(xt + m * L.xst + 16 * c) = v;
   }
-  if (threadIdx.x < 32) rn[threadIdx.x] = 0;
+  if (threadIdx.x < 32) {
+    rlo[threadIdx.x] = 1 << 20;
+    rhi[threadIdx.x] = -(1 << 20);
+    rn[threadIdx.x] = 0;
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < 32 * a.nbk; i += kThreads) {
-    const int m = i / a.nbk, kb = i - m * a.nbk;
-    int e = m < rows ? exp_from16(a.xs[(row0 + m) * a.nbk + kb]) : 0;
-    if (e == kExpNaN) {  // a NaN block makes the whole output row NaN
-      rn[m] = 1;
-      e = 0;
+  for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) {  // per row: finite min / max, NaN flag
+    const int m = i / nbk, kb = i - m * nbk;
+    const int e = m < rows ? exp_from16(a.xs[(row0 + m) * nbk + kb]) : 0;
+    if (e == kExpNaN) {
+      rn[m] = 1;  // a NaN block makes the whole output row NaN
+    } else {
+      atomicMin(&rlo[m], e);
+      atomicMax(&rhi[m], e);
     }
-    xe[kb * 32 + m] = (int16_t)e;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) {
+    const int m = i / nbk, kb = i - m * nbk;
+    const int e = m < rows ? exp_from16(a.xs[(row0 + m) * nbk + kb]) : 0;
+    const int lo = rlo[m] > rhi[m] ? 0 : rlo[m];
+    xe[kb * 32 + m] = (int16_t)(e == kExpNaN ? 0 : e - lo);
+  }
+  if (wave == 0) {  // tile stats over the 32 rows (lanes 32..63 neutral)
+    const int m = lane & 31;
+    const bool em = rlo[m] > rhi[m];
+    const int lo = em ? 0 : rlo[m], sp = em ? 0 : rhi[m] - lo;
+    const uint32_t smx = wave_reduce(lane < 32 ? (uint32_t)sp : 0u, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+    const uint32_t bmn = wave_reduce(lane < 32 ? (uint32_t)(lo + (1 << 20)) : 0xFFFFFFFFu,
+                                     [](uint32_t u, uint32_t w) { return u < w ? u : w; });
+    if (lane == 0) {
+      st[0] = (int)smx;
+      st[1] = (int)bmn - (1 << 20);
+    }
   }
   __syncthreads();
 
-  // ---- the 32 x 32 output block of this wave on int8 MFMA ----------------------
   // lane maps of v_mfma_i32_32x32x32_i8 (mxa_selftest_mfma32): A[m][k], m = lane % 32,
   // k = 16 (lane / 32) + 0..15; B[k][n], n = lane % 32; C[m][n] in c[i],
   // m = 8 (i / 4) + 4 (lane / 32) + i % 4
@@ -102,77 +223,116 @@ __global__ __launch_bounds__(64 * 3 * NBD) void qkv_proj_kernel(ProjArgs a) {
   const int ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
   const int dcol = 32 * cb + ln;
   const bool colv = dcol < D;
-  const int64_t wrow = (int64_t)s * HD + (int64_t)h * D + min(dcol, D - 1);
-  const int8_t* wp = a.wc + wrow * a.Cpad + kh;
-  const int16_t* wsp = a.ws + wrow * a.nbk;
-  double acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-  bool cnan = false;
-  v4i_ bnext = *reinterpret_cast<const v4i_*>(wp);
-  for (int kb = 0; kb < a.nbk; ++kb) {
-    const v4i_ bv = bnext;
-    if (kb + 1 < a.nbk) bnext = *reinterpret_cast<const v4i_*>(wp + 32 * (kb + 1));
-    const v4i_ av = *reinterpret_cast<const v4i_*>(xt + ln * L.xst + 32 * kb + kh);
-    const v16i zero = {};
-    const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
-    int ew = exp_from16(wsp[kb]);
-    cnan = cnan || ew == kExpNaN;
-    ew = ew == kExpNaN ? 0 : ew;
-    const int16_t* eb = xe + kb * 32 + m0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint2 e4 = *reinterpret_cast<const uint2*>(eb + 8 * q);  // rows 8q + m0 .. + 3
-      const int ex[4] = {(int)(int16_t)(e4.x & 0xFFFFu), (int)(int16_t)(e4.x >> 16), (int)(int16_t)(e4.y & 0xFFFFu),
-                         (int)(int16_t)(e4.y >> 16)};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[4 * q + r] += ldexp((double)c[4 * q + r], ex[r] + ew);
-    }
-  }
-  // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -----------
-  const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
-  const float bb = (a.bias && colv) ? round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1) : 0.0f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int m = 8 * (i >> 2) + m0 + (i & 3);
-    float o = (cnan || rn[m]) ? __uint_as_float(0x7FC00000u) : (float)acc[i];
-    o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
-    if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
-    if (colv) {
-      ot[m * L.ost + s * D + dcol] = o;
-      if (a.qkv_out && m < rows) a.qkv_out[(row0 + m) * (3 * HD) + jcol] = o;
-    }
-  }
-  __syncthreads();
+  const int8_t* xa = xt + ln * L.xst + kh;
+  const int64_t hrow_b = (int64_t)b * a.H;
 
-  // ---- q and k rows: rows_prep's per-block body on the tile (8 lanes per block) ----
-  const int64_t hrow0 = ((int64_t)b * a.H + h) * a.N + n0;  // row of (b, h, n0) in the q / k tables
-  constexpr int kTasks = 2 * 32 * NBD * 8;
-  for (int t0 = 0; t0 < kTasks; t0 += kThreads) {
-    const int t = t0 + (int)threadIdx.x;
-    const bool tv = t < kTasks;  // uniform per 8-lane group
-    const int g = t >> 3, sub = t & 7;
-    const int sk = tv ? g / (32 * NBD) : 0;
-    const int rem = tv ? g - sk * 32 * NBD : 0;
-    const int m = rem / NBD, blk = rem - m * NBD;
-    const int c0 = 32 * blk + 4 * sub;
-    float xv[4];
+  for (int h = 0; h < a.H; ++h) {
+    // ---- this wave's 32 x 32 output block of head h -------------------------------
+    const int64_t blkc = (int64_t)(s * a.H + h) * NBD + cb;  // padded 32-column block
+    const int64_t pc = 32 * blkc + ln;
+    const int8_t* wp = a.pk + (blkc * nbk) * 1024 + lane * 16;
+    const int16_t* wep = a.pe + pc * nbk;
+    const int wlo = a.ps[2 * pc], wsp = a.ps[2 * pc + 1];
+    bool cnan = false;
+    // Every block product is c * 2^(ex + ew) with |c| <= 32 * 127^2 < 2^19.  When the
+    // row and column exponent spreads sum to <= smax, the block sums shifted by
+    // (ex - rowmin) + (ew - colmin) add up exactly in int32, and one conversion gives
+    // the correctly rounded result (2 VALU per element and block).  Otherwise (or when
+    // the result could be subnormal) each block is added exactly in fp64.
+    const int wsp_max = (int)wave_max_u32((uint32_t)wsp);
+    const int wlo_min =
+        (int)wave_reduce((uint32_t)(wlo + (1 << 20)), [](uint32_t u, uint32_t w) { return u < w ? u : w; }) - (1 << 20);
+    const bool fast = st[0] + wsp_max <= a.smax && st[1] + wlo_min >= -126;
+    const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
+    const float bb = (a.bias && colv) ? round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1) : 0.0f;
+    // the K loop and the epilogue, specialised on the accumulation (FAST: shifted int32;
+    // else exact fp64): separate live ranges, so the two never hold registers together
+    auto run = [&](auto fast_c) {
+      constexpr bool FAST = decltype(fast_c)::value;
+      typename std::conditional<FAST, int, double>::type acc[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
-    rows_prep_block(sk ? a.rk : a.rq, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
-  }
-  // ---- V: cols_prep's per-column body over the 32 tokens -------------------------
-  for (int c = threadIdx.x; c < D; c += kThreads) {
-    float xv[32];
-    uint32_t mx = 0;
+      for (int i = 0; i < 16; ++i) acc[i] = 0;
+      v4i_ b0 = *reinterpret_cast<const v4i_*>(wp);
+      v4i_ b1 = nbk > 1 ? *reinterpret_cast<const v4i_*>(wp + 1024) : b0;
+      for (int kb = 0; kb < nbk; ++kb) {
+        const v4i_ bv = b0;
+        b0 = b1;
+        if (kb + 2 < nbk) b1 = *reinterpret_cast<const v4i_*>(wp + (kb + 2) * 1024);
+        const v4i_ av = *reinterpret_cast<const v4i_*>(xa + 32 * kb);
+        const v16i zero = {};
+        const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
+        int ew = exp_from16(wep[kb]);
+        cnan = cnan || ew == kExpNaN;
+        ew = ew == kExpNaN ? wlo : ew;
+        const int16_t* eb = xe + kb * 32 + m0;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const float v = j < rows ? round_bfloat(ot[j * L.ost + 2 * D + c], a.cv.bfloat, kRoundNearest, 1) : 0.0f;
-      xv[j] = v;
-      const uint32_t ub = __float_as_uint(v) & 0x7FFFFFFFu;
-      mx = ub > mx ? ub : mx;
+        for (int q = 0; q < 4; ++q) {
+          const uint2 e4 = *reinterpret_cast<const uint2*>(eb + 8 * q);  // rows 8q + m0 .. + 3
+          const int dx[4] = {(int)(e4.x & 0xFFFFu), (int)(e4.x >> 16), (int)(e4.y & 0xFFFFu), (int)(e4.y >> 16)};
+          if constexpr (FAST) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[4 * q + r] += (int)((uint32_t)c[4 * q + r] << (dx[r] + ew - wlo));
+          } else {
+            const int4 lo4 = *reinterpret_cast<const int4*>(rlo + 8 * q + m0);
+            const int lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[4 * q + r] += ldexp((double)c[4 * q + r], dx[r] + lo[r] + ew);
+          }
+        }
+      }
+      // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -------
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = 8 * (i >> 2) + m0 + (i & 3);
+        float o;
+        if constexpr (FAST) o = ldexpf((float)acc[i], rlo[m] + wlo);
+        else o = (float)acc[i];
+        if (cnan || rn[m]) o = __uint_as_float(0x7FC00000u);
+        o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+        if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
+        if (colv) {
+          ot[m * L.ost + s * D + dcol] = o;
+          if (a.qkv_out && m < rows) a.qkv_out[(row0 + m) * (3 * HD) + jcol] = o;
+        }
+      }
+    };
+    if (fast) run(std::integral_constant<bool, true>{});
+    else run(std::integral_constant<bool, false>{});
+    __syncthreads();
+
+    // ---- q and k rows: rows_prep's per-block body on the tile (8 lanes per block) ----
+    const int64_t hrow0 = (hrow_b + h) * a.N + n0;  // row of (b, h, n0) in the q / k tables
+    constexpr int kTasks = 32 * NBD * 8;            // per sub-matrix
+#pragma unroll 1
+    for (int sk = 0; sk < 2; ++sk) {  // uniform: q, then k
+      const RowsPrepArgs& ra = sk ? a.rk : a.rq;
+#pragma unroll 1
+      for (int t0 = 0; t0 < kTasks; t0 += kThreads) {
+        const int t = t0 + (int)threadIdx.x;
+        const bool tv = t < kTasks;  // uniform per 8-lane group
+        const int g = tv ? t >> 3 : 0, sub = t & 7;
+        const int m = g / NBD, blk = g - m * NBD;
+        const int c0 = 32 * blk + 4 * sub;
+        float xv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
+        rows_prep_block(ra, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
+      }
     }
-    cols_prep_column(a.cv, (int64_t)b * a.H + h, tb, c, xv, mx);
+    // ---- V: cols_prep's per-column body over the 32 tokens -------------------------
+    for (int c = threadIdx.x; c < D; c += kThreads) {
+      float xv[32];
+      uint32_t mx = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const float v = j < rows ? round_bfloat(ot[j * L.ost + 2 * D + c], a.cv.bfloat, kRoundNearest, 1) : 0.0f;
+        xv[j] = v;
+        const uint32_t ub = __float_as_uint(v) & 0x7FFFFFFFu;
+        mx = ub > mx ? ub : mx;
+      }
+      cols_prep_column(a.cv, hrow_b + h, tb, c, xv, mx);
+    }
+    __syncthreads();
   }
 }
 

@@ -298,17 +298,22 @@ def mx_approx_scores(q: torch.Tensor, k: torch.Tensor, pred_mode: str = "ex_pred
 
 class LinearWeightMX:
     """A Linear weight (out_features, in_features) as MXINT8 codes + block exponents
-    along in_features on the device (mxa_linear_weight_prep): prepared once, reused by
-    every fused call (the weights are constant at inference)."""
+    along in_features on the device (mxa_linear_weight_prep), MFMA-ready in column
+    groups of group_width (qkv: the head dim): prepared once, reused by every fused
+    call (the weights are constant at inference)."""
 
-    def __init__(self, weight: torch.Tensor, flush_subnormals: bool = False, bfloat: int = 0):
+    def __init__(self, weight: torch.Tensor, group_width: int, flush_subnormals: bool = False, bfloat: int = 0):
         dev = require_device(weight)
         w = _f32(weight.detach(), "weight").contiguous()
         self.out_features, self.in_features = w.shape
-        nbytes = lib().mxa_linear_weight_bytes(self.out_features, self.in_features)
+        self.group_width = int(group_width)
+        nbytes = lib().mxa_linear_weight_bytes(self.out_features, self.in_features, self.group_width)
+        if nbytes < 0:
+            raise ValueError(f"group_width {group_width} does not divide out_features {self.out_features}")
         self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        check(lib().mxa_linear_weight_prep(w.data_ptr(), self.out_features, self.in_features, int(bool(flush_subnormals)),
-                                           int(bfloat), self.buf.data_ptr(), stream_ptr(dev)), "mxa_linear_weight_prep")
+        check(lib().mxa_linear_weight_prep(w.data_ptr(), self.out_features, self.in_features, self.group_width,
+                                           int(bool(flush_subnormals)), int(bfloat), self.buf.data_ptr(),
+                                           stream_ptr(dev)), "mxa_linear_weight_prep")
         self.flush, self.bfloat = bool(flush_subnormals), int(bfloat)
 
 
@@ -324,12 +329,16 @@ def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_
     if x.dim() != 3 or x.stride(2) != 1:
         raise ValueError("x must be (B, N, C) with contiguous C")
     B, Ntok, C = x.shape
-    wq = weight if isinstance(weight, LinearWeightMX) else LinearWeightMX(weight, flush_subnormals, bfloat)
-    if wq.in_features != C or wq.out_features % (3 * num_heads):
-        raise ValueError(f"weight ({wq.out_features}, {wq.in_features}) does not fit x C={C}, heads={num_heads}")
+    out_f = weight.out_features if isinstance(weight, LinearWeightMX) else weight.shape[0]
+    if out_f % (3 * num_heads):
+        raise ValueError(f"weight rows {out_f} are not 3 * heads * head_dim")
+    D = out_f // (3 * num_heads)
+    wq = weight if isinstance(weight, LinearWeightMX) else LinearWeightMX(weight, D, flush_subnormals, bfloat)
+    if wq.in_features != C or wq.group_width != D:
+        raise ValueError(f"weight ({wq.out_features}, {wq.in_features}) / group {wq.group_width} does not fit "
+                         f"x C={C}, heads={num_heads}")
     if (wq.flush, wq.bfloat) != (bool(flush_subnormals), int(bfloat)):
         raise ValueError("the prepared weight was quantized with other flush / bfloat settings")
-    D = wq.out_features // (3 * num_heads)
     if top_k and not (0 < k_top <= Ntok):
         raise ValueError(f"k={k_top} out of range for {Ntok} keys")
     if approx and top_k and pred_mode not in N.PRED_MODES:

@@ -524,7 +524,7 @@ def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
         from mx_quantization_amd.funcs import _create_structured_orthogonal_matrix
         torch.manual_seed(D)
         proj = _create_structured_orthogonal_matrix(D).numpy()
-    wq = M.LinearWeightMX(dev(W))
+    wq = M.LinearWeightMX(dev(W), D)
     out, idx, qkv = M.mx_qkv_attention(dev(x), wq, dev(bias), H, D ** -0.5, k_top=k, pred_mode=mode,
                                        return_qkv=True, elsa_proj=None if proj is None else dev(proj))
     torch.cuda.synchronize()
