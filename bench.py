@@ -59,12 +59,16 @@ CONFIGS = {
     "pixart_cross": dict(workload="PixArt-alpha 256x256 cross-attention core, MXINT4 (Sanger) approximator",
                          B=8, H=16, N=256, T=120, D=72, k=20, mode="MXINT4", scale=1 / np.sqrt(72), bias=True),
 }
-STAGES = ("rows_prep_q", "rows_prep_k", "cols_prep_v", "select", "finish")  # mxa_attention_timed order
-QKV_STAGES = ("-", "x_quant+qkv_proj", "-", "select", "finish")  # mxa_qkv_attention_timed order
+# bench stages <- mxa_attention_timed's stage slots (include/mxa.h: 0 the operand builders
+# for Q, K and V in one launch; 1, 2 empty; 3 selection; 4 finishing / dense row kernel)
+STAGES = ("prep", "select", "finish")
+STAGE_SLOTS = (0, 3, 4)
+QKV_STAGES = ("x_quant+qkv_proj", "select", "finish")  # mxa_qkv_attention_timed, same slots
 
 
 def stage_bytes(c, path):
     """Algorithmic HBM bytes each kernel must move per launch:
+      prep    the operand builders (Q, K rows, V columns: one launch)
       select  selection kernel (approximate scores + top-k; writes the kept indices)
       finish  finishing kernel (gather, softmax, P, P.V; writes out)  [dense path: the row kernel]"""
     h = c["B"] * c["H"]
@@ -79,11 +83,7 @@ def stage_bytes(c, path):
     else:  # approximator codes + int16 block scales
         apx = lambda rows: rows * (dpad + 2 * nbd)
     vtab = D * tpad + 2 * ntb * D
-    by = {
-        "rows_prep_q": h * (4 * N * D + codes(N) + apx(N)),
-        "rows_prep_k": h * (4 * T * D + codes(T) + apx(T)),
-        "cols_prep_v": h * (4 * T * D + vtab),
-    }
+    by = {"prep": h * (4 * N * D + codes(N) + apx(N)) + h * (4 * T * D + codes(T) + apx(T)) + h * (4 * T * D + vtab)}
     if path == "rows_split":
         by["select"] = h * (apx(N) + apx(T) + 8 * N * k + 4 * N * k)
         by["finish"] = h * (codes(N) + codes(T) + vtab + 4 * N * k + 4 * N * D)
@@ -258,7 +258,7 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
         lambda: N.check(N.lib().mxa_attention_timed(ctypes.byref(p), stream, steps, stage_ms), "mxa_attention_timed"),
         world, torch.cuda.synchronize, device)
     path = N.PATH_NAMES.get(N.lib().mxa_attention_path(ctypes.byref(p)), "?")
-    stages = {STAGES[i]: float(stage_ms[i]) for i in range(len(STAGES))}
+    stages = {name: float(stage_ms[slot]) for name, slot in zip(STAGES, STAGE_SLOTS)}
     cb = dict(c, B=B)
     by = stage_bytes(cb, path)
     dom = max(stages, key=stages.get)
@@ -266,7 +266,7 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
     traffic = None
     if traffic_json and os.path.exists(traffic_json):
         traffic = json.load(open(traffic_json)).get(dom)
-    qa_ms = stages["rows_prep_q"] + stages["rows_prep_k"] + stages["cols_prep_v"] + stages["select"]
+    qa_ms = stages["prep"] + stages["select"]
     qa_gbs = bytes_qa(cb) / (qa_ms * 1e-3) / 1e9
     mf_tops = ops_gemm(cb) / (stages["finish"] * 1e-3) / 1e12
     roof = {
@@ -329,7 +329,7 @@ def run_qkv(c, images, steps, warmup, device, world):
     elapsed = timed_region(
         lambda: N.check(N.lib().mxa_qkv_attention_timed(ctypes.byref(p), ctypes.byref(xp), stream, steps, stage_ms),
                         "mxa_qkv_attention_timed"), world, torch.cuda.synchronize, device)
-    stages = {QKV_STAGES[i]: float(stage_ms[i]) for i in range(5) if QKV_STAGES[i] != "-"}
+    stages = {name: float(stage_ms[slot]) for name, slot in zip(QKV_STAGES, STAGE_SLOTS)}
     proj_ms = stages["x_quant+qkv_proj"]
     ops = 2 * B * Nt * C * 3 * C  # int8 ops of the projection GEMM
     extra = {"proj_int8_tops": ops / (proj_ms * 1e-3) / 1e12,

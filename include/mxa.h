@@ -186,8 +186,9 @@ int mxa_attention_path(const mxa_attn_params* p);
  * Measurement entry point (bench.py): runs mxa_attention `iters` times on `stream`
  * recording HIP events between the kernels, synchronizes the stream, and writes
  * the mean milliseconds of each stage to stage_ms[MXA_ATTN_STAGES]:
- *   0 rows_prep(Q)  1 rows_prep(K)  2 cols_prep(V)  3 scores+top-k (the whole fused row kernel
- *   on MXA_PATH_ROWS_FUSED)  4 gather+softmax+P+P.V (0 on MXA_PATH_ROWS_FUSED)
+ *   0 the operand builders (Q, K rows and V columns, one launch; for mxa_qkv_attention_timed
+ *   the x quantization + projection)  1, 2 empty  3 scores+top-k (on MXA_PATH_ROWS_FUSED: 0)
+ *   4 gather+softmax+P+P.V (on MXA_PATH_ROWS_FUSED: the dense row kernel)
  * Host-synchronizing: not for use inside graph capture.
  */
 #define MXA_ATTN_STAGES 5

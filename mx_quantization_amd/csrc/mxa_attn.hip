@@ -467,11 +467,6 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   rq.signs = mode == kModeExSign ? reinterpret_cast<uint32_t*>(ws + L.qsg) : nullptr;
   rq.sA = need_sa ? reinterpret_cast<int16_t*>(ws + L.qsA) : nullptr;
   if (ev) (void)hipEventRecord(ev[0], stream);
-  if (!xq) {
-    rc = launch_rows_prep(rq, stream);
-    if (rc) return rc;
-  }
-  if (ev) (void)hipEventRecord(ev[1], stream);
 
   RowsPrepArgs rk = rq;
   rk.x = pp.k; rk.s0 = pp.k_strides[0]; rk.s1 = pp.k_strides[1]; rk.s2 = pp.k_strides[2];
@@ -492,8 +487,11 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
   if (xq) {
     rc = launch_qkv_proj(pp, *xq, L, rq, rk, cv, ws, stream);
+  } else if (scores_only) {
+    rc = launch_rows_prep(rq, stream);
+    if (!rc) rc = launch_rows_prep(rk, stream);
   } else {
-    rc = launch_rows_prep(rk, stream);
+    rc = launch_attn_prep(rq, rk, cv, stream);  // Q, K and V in one launch
   }
   if (rc) return rc;
   if (mode == kModeElsa) {  // hashes of MX(Q), MX(K); norms of MX(K) rows
@@ -510,13 +508,11 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     rc = launch_elsa_prep(ek, stream);
     if (rc) return rc;
   }
-  if (ev) (void)hipEventRecord(ev[2], stream);
-
-  if (!scores_only && !xq) {
-    rc = launch_cols_prep(cv, stream);
-    if (rc) return rc;
+  if (ev) {  // stages 1 and 2 are empty: the operand builders run as stage 0
+    (void)hipEventRecord(ev[1], stream);
+    (void)hipEventRecord(ev[2], stream);
+    (void)hipEventRecord(ev[3], stream);
   }
-  if (ev) (void)hipEventRecord(ev[3], stream);
 
   r2.qc = reinterpret_cast<const int8_t*>(ws + L.qc);
   r2.qop = reinterpret_cast<const int8_t*>(ws + L.qop);

@@ -73,6 +73,8 @@ struct ColsPrepArgs {
 
 int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream);
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream);
+// Q rows, K rows and V columns of the attention path in one launch
+int launch_attn_prep(const RowsPrepArgs& q, const RowsPrepArgs& k, const ColsPrepArgs& v, hipStream_t stream);
 int launch_elsa_prep(const ElsaPrepArgs& a, hipStream_t stream);
 
 typedef int v4i __attribute__((ext_vector_type(4)));

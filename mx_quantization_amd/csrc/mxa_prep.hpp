@@ -19,59 +19,72 @@ __device__ __forceinline__ int exion_m(int raw) {
   return p1 + (t > 0 ? (1 << (31 - __clz(t))) : 0);
 }
 
-// One 32-element block of a row, 8 lanes x 4 elements (lane sub = 0..7 of an
-// 8-lane group, c0 = 32 blk + 4 sub): MXINT8 codes, block exponent, approximator
-// operand and sign word into the RowsPrepArgs outputs (row `row`, block `blk`).
-// The 8 lanes of a group must be consecutive and all call it (DPP reductions).
+// reduction over the LPB consecutive lanes that share one 32-element block
+template <int LPB, class Op>
+__device__ __forceinline__ uint32_t blk_reduce(uint32_t v, Op op) {
+  v = op(v, dpp_u32<0xB1>(v));  // quad_perm [1,0,3,2]
+  if constexpr (LPB >= 4) v = op(v, dpp_u32<0x4E>(v));   // quad_perm [2,3,0,1]
+  if constexpr (LPB >= 8) v = op(v, dpp_u32<0x141>(v));  // row_half_mirror
+  return v;
+}
+
+// One 32-element block of a row, 32/EPL lanes x EPL elements (lane sub of its group,
+// c0 = 32 blk + EPL sub): MXINT8 codes, block exponent, approximator operand and sign
+// word into the RowsPrepArgs outputs (row `row`, block `blk`).  The lanes of a group
+// must be consecutive and all call it (DPP reductions).  EPL = 16: the standalone
+// prep (two lanes per block: the per-block work is shared by 2 lanes, not 8);
+// EPL = 4: the fused projection's tile epilogue.
+template <int EPL>
 __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t row, int blk, int sub, int c0,
-                                                float xv[4], bool valid) {
+                                                float xv[EPL], bool valid) {
+  constexpr int LPB = 32 / EPL;
   uint32_t mb = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < EPL; ++j) {
     xv[j] = round_bfloat(xv[j], a.bfloat, kRoundNearest, 1);
     const uint32_t ub = __float_as_uint(xv[j]) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;
   }
-  mb = oct_reduce(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  mb = blk_reduce<LPB>(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   int e_raw;
   const int es = scale_exponent(mb, 127, &e_raw);
   const bool nanblk = es == kExpNaN;
   if (a.flush && !(e_raw != kExpNaN && e_raw > -127)) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] = xv[j] * 0.0f;
+    for (int j = 0; j < EPL; ++j) xv[j] = xv[j] * 0.0f;
   }
-  int code[4];
+  int code[EPL];
   int maxc = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < EPL; ++j) {
     code[j] = nanblk ? 0 : (int)round_code(xv[j], es, 8, kRoundNearest);
     const int ac = code[j] < 0 ? -code[j] : code[j];
     maxc = ac > maxc ? ac : maxc;
   }
-  maxc = (int)oct_reduce((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  maxc = (int)blk_reduce<LPB>((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
   // floor(log2(max |MX|)), unclamped; MX max = maxc * 2^(es-6) exactly.
   int eA;
   if (nanblk) eA = kExpNaN;
   else if (maxc == 0) eA = -126;
   else eA = floor_log2_pos((float)maxc * pow2f(es - 6));
-  int op[4];
+  int op[EPL];
   int sA;
   switch (a.op_kind) {
     case MXA_OP_SIGN:
 #pragma unroll
-      for (int j = 0; j < 4; ++j) op[j] = (c0 + j < a.D) ? (code[j] < 0 ? -1 : 1) : 0;
+      for (int j = 0; j < EPL; ++j) op[j] = (c0 + j < a.D) ? (code[j] < 0 ? -1 : 1) : 0;
       sA = eA;
       break;
     case MXA_OP_MXINT4:
 #pragma unroll
-      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest);
+      for (int j = 0; j < EPL; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest);
       sA = nanblk ? kExpNaN : es - 2;
       break;
     case MXA_OP_EXION: {
       const int sh = nanblk ? 0 : es - eA;  // MX / 2^eA * 64 = code * 2^(es-eA), an integer < 128
 #pragma unroll
-      for (int j = 0; j < 4; ++j) op[j] = nanblk ? 0 : exion_m(code[j] << sh);
+      for (int j = 0; j < EPL; ++j) op[j] = nanblk ? 0 : exion_m(code[j] << sh);
       sA = eA;
       break;
     }
@@ -80,7 +93,7 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       // (mx < 0 ? -1 : 1) * 2^floor(log2|mx|), zeros -> +1.  Nonzero elements as the
       // power-of-two code sign * 2^floor(log2|code|) in units of 2^(es-6); zeros in zind
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < EPL; ++j) {
         const int ac = code[j] < 0 ? -code[j] : code[j];
         const int p2 = ac ? 1 << (31 - __clz(ac)) : 0;
         op[j] = code[j] < 0 ? -p2 : p2;
@@ -91,38 +104,45 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       break;
     default:  // MXA_OP_MXINT8
 #pragma unroll
-      for (int j = 0; j < 4; ++j) op[j] = code[j];
+      for (int j = 0; j < EPL; ++j) op[j] = code[j];
       sA = nanblk ? kExpNaN : es - 6;
       break;
   }
   if (valid) {
     const int64_t base = row * a.dpad + c0;
-    const uint32_t pc = (uint32_t)(code[0] & 0xFF) | ((uint32_t)(code[1] & 0xFF) << 8) |
-                        ((uint32_t)(code[2] & 0xFF) << 16) | ((uint32_t)(code[3] & 0xFF) << 24);
-    const uint32_t po = (uint32_t)(op[0] & 0xFF) | ((uint32_t)(op[1] & 0xFF) << 8) |
-                        ((uint32_t)(op[2] & 0xFF) << 16) | ((uint32_t)(op[3] & 0xFF) << 24);
-    if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc;
-    if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po;
-    if (a.zind) {
-      uint32_t pz = 0u;
+    uint32_t pc[EPL / 4], po[EPL / 4], pz[EPL / 4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pz |= (c0 + j < a.D && code[j] == 0 ? 1u : 0u) << (8 * j);
-      *reinterpret_cast<uint32_t*>(a.zind + base) = pz;
+    for (int w = 0; w < EPL / 4; ++w) {
+      pc[w] = po[w] = pz[w] = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pc[w] |= (uint32_t)(code[4 * w + j] & 0xFF) << (8 * j);
+        po[w] |= (uint32_t)(op[4 * w + j] & 0xFF) << (8 * j);
+        pz[w] |= (c0 + 4 * w + j < a.D && code[4 * w + j] == 0 ? 1u : 0u) << (8 * j);
+      }
+    }
+    if constexpr (EPL == 16) {
+      if (a.codes) *reinterpret_cast<uint4*>(a.codes + base) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+      if (a.op) *reinterpret_cast<uint4*>(a.op + base) = make_uint4(po[0], po[1], po[2], po[3]);
+      if (a.zind) *reinterpret_cast<uint4*>(a.zind + base) = make_uint4(pz[0], pz[1], pz[2], pz[3]);
+    } else {
+      if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc[0];
+      if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po[0];
+      if (a.zind) *reinterpret_cast<uint32_t*>(a.zind + base) = pz[0];
     }
   }
-  // packed sign word of the block, bit (4*sub + j) = (code < 0): the exp-sign
+  // packed sign word of the block, bit (EPL*sub + j) = (code < 0): the exp-sign
   // operand of ex_pred (codes beyond D are 0, i.e. positive)
   uint32_t sw = 0u;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) sw |= (code[j] < 0 ? 1u : 0u) << (4 * sub + j);
-  sw = oct_reduce(sw, [](uint32_t u, uint32_t w) { return u | w; });
+  for (int j = 0; j < EPL; ++j) sw |= (code[j] < 0 ? 1u : 0u) << (EPL * sub + j);
+  sw = blk_reduce<LPB>(sw, [](uint32_t u, uint32_t w) { return u | w; });
   if (valid && sub == 0) {
     if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
     if (a.sA) a.sA[row * a.nb + blk] = exp_to16(sA);
     if (a.signs) a.signs[row * a.nb + blk] = sw;
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // operand builder for matrices quantized along the row axis (V, and in2 of

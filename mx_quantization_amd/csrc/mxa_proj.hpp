@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
         float xv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
-        rows_prep_block(ra, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
+        rows_prep_block<4>(ra, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
       }
     }
     // ---- V: cols_prep's per-column body over the 32 tokens -------------------------

@@ -114,12 +114,13 @@ __global__ __launch_bounds__(256) void bfloat_kernel(const float* __restrict__ x
 // attention operand builder for rows quantized along the last axis (Q, K):
 // 8 lanes per 32-element block, 4 floats (16 B) per lane (body: mxa_prep.hpp)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
-  // 32-bit index math (the launcher checks rows * nb < 2^31): a 64-bit division
-  // is a ~50-instruction software sequence per thread, 32-bit ~10
-  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int sub = threadIdx.x & 7;
-  const uint32_t g = gt >> 3;
+__device__ __forceinline__ void rows_prep_body(const RowsPrepArgs& a, uint32_t bid) {
+  // two lanes per 32-element block, 16 floats (4 x 16 B) per lane; 32-bit index math
+  // (the launcher checks rows * nb < 2^31): a 64-bit division is a ~50-instruction
+  // software sequence per thread, 32-bit ~10
+  const uint32_t gt = bid * 256u + threadIdx.x;
+  const int sub = threadIdx.x & 1;
+  const uint32_t g = gt >> 1;
   const uint32_t ngroups = (uint32_t)(a.rows * a.nb);
   const bool valid = g < ngroups;
   const uint32_t nb = (uint32_t)a.nb, R = (uint32_t)a.R, H = (uint32_t)a.H;
@@ -132,25 +133,29 @@ __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) {
   const int64_t h = bh32 - b32 * H;
   const int64_t b = b32;
   const float* xr = a.x + b * a.s0 + h * a.s1 + r * a.s2;
-  const int c0 = blk * 32 + sub * 4;
-  float xv[4];
-  if (valid && a.vec4 && c0 + 4 <= a.D) {
-    const float4 v = *reinterpret_cast<const float4*>(xr + c0);
-    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
+  const int c0 = blk * 32 + sub * 16;
+  float xv[16];
+  if (valid && a.vec4 && c0 + 16 <= a.D) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(xr + c0 + 4 * q);
+      xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
+    }
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] = (valid && c0 + j < a.D) ? xr[c0 + j] : 0.0f;
+    for (int j = 0; j < 16; ++j) xv[j] = (valid && c0 + j < a.D) ? xr[c0 + j] : 0.0f;
   }
-  rows_prep_block(a, row, blk, sub, c0, xv, valid);
+  rows_prep_block<16>(a, row, blk, sub, c0, xv, valid);
 }
+__global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) { rows_prep_body(a, blockIdx.x); }
 
 // ---------------------------------------------------------------------------
 // operand builder for matrices quantized along the row axis (V, and in2 of
 // mx.matmul): one thread per (matrix, block, column), coalesced along columns
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) {
+__device__ __forceinline__ void cols_prep_body(const ColsPrepArgs& a, uint32_t bid) {
   // 32-bit index math (the launcher checks the thread count fits)
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = bid * 256u + threadIdx.x;
   const uint32_t total = (uint32_t)(a.mats * a.nb * a.C);
   if (t >= total) return;
   const uint32_t C = (uint32_t)a.C, NB = (uint32_t)a.nb, H = (uint32_t)a.H;
@@ -176,6 +181,18 @@ __global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) {
     mx = ub > mx ? ub : mx;
   }
   cols_prep_column(a, m, blk, c, xv, mx);
+}
+__global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) { cols_prep_body(a, blockIdx.x); }
+
+// The attention path's three operand builders in ONE launch (no launch gaps / tails
+// between them): blocks [0, nq) quantize Q rows, [nq, nq + nk) K rows, the rest V
+// columns.  The role is uniform per workgroup.
+__global__ __launch_bounds__(256) void attn_prep_kernel(RowsPrepArgs q, RowsPrepArgs k, ColsPrepArgs v, uint32_t nq,
+                                                        uint32_t nk) {
+  const uint32_t b = blockIdx.x;
+  if (b < nq) rows_prep_body(q, b);
+  else if (b < nq + nk) rows_prep_body(k, b - nq);
+  else cols_prep_body(v, b - nq - nk);
 }
 
 // ---------------------------------------------------------------------------
@@ -360,9 +377,9 @@ extern "C" int mxa_approx_values(const float* x, float* out, int64_t rows, int32
 
 namespace mxa {
 int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream) {
-  const int64_t threads = a.rows * a.nb * 8;
+  const int64_t threads = a.rows * a.nb * 2;
   if (threads == 0) return MXA_OK;
-  if (a.rows * a.nb >= ((int64_t)1 << 28)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices (x8 lanes)
+  if (a.rows * a.nb >= ((int64_t)1 << 30)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices (x2 lanes)
   hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
@@ -375,6 +392,17 @@ int launch_elsa_prep(const ElsaPrepArgs& a, hipStream_t stream) {
     return MXA_ERR_LAUNCH;
   const int64_t blocks = std::min<int64_t>((a.rows + kElsaWaves - 1) / kElsaWaves, 2048);
   hipLaunchKernelGGL(elsa_prep_kernel, dim3((unsigned)blocks), dim3(64 * kElsaWaves), lds, stream, a);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+int launch_attn_prep(const RowsPrepArgs& q, const RowsPrepArgs& k, const ColsPrepArgs& v, hipStream_t stream) {
+  if (q.rows * q.nb >= ((int64_t)1 << 30) || k.rows * k.nb >= ((int64_t)1 << 30) ||
+      v.mats * v.nb * v.C >= ((int64_t)1 << 31))
+    return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices
+  const int64_t nq = (q.rows * q.nb * 2 + 255) / 256, nk = (k.rows * k.nb * 2 + 255) / 256;
+  const int64_t nv = (v.mats * v.nb * v.C + 255) / 256;
+  if (nq + nk + nv == 0) return MXA_OK;
+  hipLaunchKernelGGL(attn_prep_kernel, dim3((unsigned)(nq + nk + nv)), dim3(256), 0, stream, q, k, v, (uint32_t)nq,
+                     (uint32_t)nk);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream) {

@@ -124,7 +124,8 @@ def test_hbm_traffic_kernel_names_map_to_bench_stages():
     ht = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ht)
     assert ht.stage_of("void mxa::select_kernel<256, 3>(mxa::Rows2Args)") == "select"
-    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 3, true, false, 2>(mxa::Rows2Args)") == "finish"
-    assert ht.stage_of("void mxa::attn_rows2_kernel<4, 0, false, false, 0>(mxa::Rows2Args)") == "finish"
-    assert ht.stage_of("mxa::rows_prep_kernel(mxa::RowsPrepArgs)") == "rows_prep"
-    assert ht.stage_of("mxa::cols_prep_kernel(mxa::ColsPrepArgs)") == "cols_prep_v"
+    assert ht.stage_of("void mxa::finish_kernel<2, 2>(mxa::Rows2Args)") == "finish"
+    assert ht.stage_of("void mxa::dense_rows_kernel<4>(mxa::Rows2Args)") == "finish"
+    assert ht.stage_of("mxa::attn_prep_kernel(mxa::RowsPrepArgs, mxa::RowsPrepArgs, mxa::ColsPrepArgs, unsigned int, "
+                       "unsigned int)") == "prep"
+    assert ht.stage_of("void mxa::qkv_proj_kernel<2>(mxa::ProjArgs)") == "proj"

@@ -17,12 +17,12 @@ import sys
 def stage_of(kernel):
     if "select_kernel" in kernel:
         return "select"
-    if "attn_rows2_kernel" in kernel:  # template <S, MODE, TOPK, BIG, PART>: 2 finishing, 0 dense
+    if "finish_kernel" in kernel or "dense_rows_kernel" in kernel:
         return "finish"
-    if "rows_prep_kernel" in kernel:
-        return "rows_prep"
-    if "cols_prep_kernel" in kernel:
-        return "cols_prep_v"
+    if "attn_prep_kernel" in kernel or "rows_prep_kernel" in kernel or "cols_prep_kernel" in kernel:
+        return "prep"
+    if "qkv_proj_kernel" in kernel:
+        return "proj"
     return None
 
 
@@ -44,9 +44,6 @@ def main():
     out = {}
     for st in set(fetch) | set(write):
         out[st] = 2.0 * fetch.get(st, 0.0) + write.get(st, 0.0)
-    # rows_prep runs twice per step (Q, K): report each launch
-    if "rows_prep" in out:
-        out["rows_prep_q"] = out["rows_prep_k"] = out.pop("rows_prep")
     out["_raw"] = {"fetch_bytes_x1": fetch, "write_bytes": write,
                    "note": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 correction"}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
