@@ -300,24 +300,22 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
     else run(std::integral_constant<bool, false>{});
     __syncthreads();
 
-    // ---- q and k rows: rows_prep's per-block body on the tile (8 lanes per block) ----
+    // ---- q and k rows: rows_prep's per-block body on the tile (2 lanes per block) ----
     const int64_t hrow0 = (hrow_b + h) * a.N + n0;  // row of (b, h, n0) in the q / k tables
-    constexpr int kTasks = 32 * NBD * 8;            // per sub-matrix
+    constexpr int kPer = 32 * NBD * 2;              // lanes per sub-matrix: a multiple of 64
 #pragma unroll 1
-    for (int sk = 0; sk < 2; ++sk) {  // uniform: q, then k
-      const RowsPrepArgs& ra = sk ? a.rk : a.rq;
-#pragma unroll 1
-      for (int t0 = 0; t0 < kTasks; t0 += kThreads) {
-        const int t = t0 + (int)threadIdx.x;
-        const bool tv = t < kTasks;  // uniform per 8-lane group
-        const int g = tv ? t >> 3 : 0, sub = t & 7;
-        const int m = g / NBD, blk = g - m * NBD;
-        const int c0 = 32 * blk + 4 * sub;
-        float xv[4];
+    for (int t0 = 0; t0 < 2 * kPer; t0 += kThreads) {
+      const int t = t0 + (int)threadIdx.x;
+      const bool tv = t < 2 * kPer;
+      const int sk = __builtin_amdgcn_readfirstlane(tv ? t / kPer : 0);  // uniform per wave: q or k
+      const int rem = tv ? t - sk * kPer : 0;
+      const int g = rem >> 1, sub = rem & 1;
+      const int m = g / NBD, blk = g - m * NBD;
+      const int c0 = 32 * blk + 16 * sub;
+      float xv[16];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
-        rows_prep_block<4>(ra, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
-      }
+      for (int j = 0; j < 16; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
+      rows_prep_block<16>(sk ? a.rk : a.rq, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
     }
     // ---- V: cols_prep's per-column body over the 32 tokens -------------------------
     for (int c = threadIdx.x; c < D; c += kThreads) {
