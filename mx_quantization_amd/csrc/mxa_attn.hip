@@ -263,9 +263,12 @@ static int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stre
 }
 
 // ---- finishing kernel (mxa_finish.hpp): 32-row MFMA tiles, one per wave ------------
+// two lanes per query row (one pass per tile) when every row's kept keys fit 2 x 16 slots
+static bool finish_pair(const Rows2Args& ra) { return ra.k_top <= 32; }
 static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg) {
   const int tiles = (ra.N + kFinTile - 1) / kFinTile;
-  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w).total; };
+  const bool pair = finish_pair(ra);
+  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, pair).total; };
   if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   // a head's tiles round-robin over the waves of one workgroup (the K / V tables
   // staged once per head); few heads (PixArt cross-attention): the tiles split over
@@ -291,28 +294,36 @@ static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg
   *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
   return MXA_OK;
 }
-template <int NB, int KS>
+template <int NB, int KS, bool PAIR>
 static int launch_finish_ks(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
   int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
-  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS>),
+  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish_kernel<NB, KS>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 template <int NB>
 static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (finish_pair(ra)) {  // slots per lane: ceil(k / 2)
+    const int kp = (ra.k_top + 1) / 2;
+    if (kp <= 2) return launch_finish_ks<NB, 2, true>(ra, BH, stream);
+    if (kp <= 4) return launch_finish_ks<NB, 4, true>(ra, BH, stream);
+    if (kp <= 8) return launch_finish_ks<NB, 8, true>(ra, BH, stream);
+    if (kp <= 12) return launch_finish_ks<NB, 12, true>(ra, BH, stream);
+    return launch_finish_ks<NB, 16, true>(ra, BH, stream);
+  }
   const int ks = (ra.k_top + 15) / 16;
-  if (ks <= 1) return launch_finish_ks<NB, 1>(ra, BH, stream);
-  if (ks <= 2) return launch_finish_ks<NB, 2>(ra, BH, stream);
-  if (ks <= 4) return launch_finish_ks<NB, 4>(ra, BH, stream);
-  if (ks <= 8) return launch_finish_ks<NB, 8>(ra, BH, stream);
-  if (ks <= 16) return launch_finish_ks<NB, 16>(ra, BH, stream);
-  return launch_finish_ks<NB, 32>(ra, BH, stream);
+  if (ks <= 1) return launch_finish_ks<NB, 1, false>(ra, BH, stream);
+  if (ks <= 2) return launch_finish_ks<NB, 2, false>(ra, BH, stream);
+  if (ks <= 4) return launch_finish_ks<NB, 4, false>(ra, BH, stream);
+  if (ks <= 8) return launch_finish_ks<NB, 8, false>(ra, BH, stream);
+  if (ks <= 16) return launch_finish_ks<NB, 16, false>(ra, BH, stream);
+  return launch_finish_ks<NB, 32, false>(ra, BH, stream);
 }
 static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
   if (plan) {

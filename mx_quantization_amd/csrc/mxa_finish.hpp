@@ -36,7 +36,7 @@ typedef int v4i_ __attribute__((ext_vector_type(4)));
 struct FinLds {
   size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
 };
-__host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves) {
+__host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves, bool pair) {
   FinLds L;
   size_t o = 0;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -51,7 +51,7 @@ __host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vs
   L.waves = o;
   L.sp = al((size_t)kFinTile * vst);
   L.bm = L.sp + al((size_t)ntb * kFinTile * 4);
-  L.per_wave = L.bm + 4 * 16 * 4;
+  L.per_wave = L.bm + (pair ? 32 : 4) * 16 * 4;  // block maxima: 16 per row of a pass
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
@@ -61,8 +61,13 @@ __device__ __forceinline__ float scale_f(int e) {
   return e == kExpNaN ? __uint_as_float(0x7FC00000u) : (e < -149 ? 0.0f : pow2f(e));
 }
 
-// NB: 32-blocks per head dim (nbd); KS: kept slots per lane (k <= 16 KS)
-template <int NB, int KS>
+// NB: 32-blocks per head dim (nbd); KS: kept slots per lane.
+// PAIR = false: eight passes of four rows per tile, one 16-lane DPP row per query row
+//   (k <= 16 KS; DiT's k = 154);
+// PAIR = true: the tile's 32 rows in ONE pass, two lanes per query row (k <= 2 KS <= 32,
+//   DeiT's k = 20): every lane busy, one round of softmax / MX(P) synchronisation per
+//   tile instead of eight.
+template <int NB, int KS, bool PAIR>
 __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   const int T = a.T, D = a.D, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
   constexpr int nbd = NB;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves);
+  const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves, PAIR);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
   int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
@@ -78,7 +83,8 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   unsigned char* wb = smem + L.waves + (size_t)wave * L.per_wave;
   int8_t* ptile = reinterpret_cast<int8_t*>(wb);
   float* sP = reinterpret_cast<float*>(wb + L.sp);
-  uint32_t* bm = reinterpret_cast<uint32_t*>(wb + L.bm) + 16 * gi;
+  // block maxima of the P row being quantized: 16 words per row (T <= 512)
+  uint32_t* bm = reinterpret_cast<uint32_t*>(wb + L.bm) + 16 * (PAIR ? (lane >> 1) : gi);
 
   // ---- stage the head's K and V tables; clear the code tile -----------------------
   const int64_t kb = (int64_t)bh * T;
@@ -100,20 +106,51 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
     const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
     for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tve[i] = vssrc[i];
     for (int i = lane; i < kFinTile * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
-    bm[gl] = 0u;
+    if (PAIR) {
+      for (int i = lane & 1; i < 16; i += 2) bm[i] = 0u;
+    } else {
+      bm[gl] = 0u;
+    }
   }
   __syncthreads();
 
   const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
-  // a pass's global inputs (the row's query codes / exponents and kept indices),
-  // loaded one pass ahead so that their latency hides behind the previous pass
-  struct PassIn {
+
+    // a pass's global inputs (the row's query codes / exponents and kept indices),
+    // loaded one pass ahead so that their latency hides behind the previous pass
+    struct PassIn {
+      uint4 qv[2 * NB];
+      int qe[NB];
+      int ix[KS];
+    };
+    auto load_pass = [&](int r0, int pass, PassIn& in) {
+      const int r = r0 + 4 * pass + gi;
+      const bool valid = r < r_end;
+      const int64_t grow = (int64_t)bh * a.N + (valid ? r : r_beg);
+      const int8_t* qsrc = a.qc + grow * a.dpad;
+  #pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        in.qv[2 * b] = *reinterpret_cast<const uint4*>(qsrc + 32 * b);
+        in.qv[2 * b + 1] = *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16);
+        in.qe[b] = exp_from16(a.qsT[grow * nbd + b]);
+      }
+  #pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        const int s = gl + 16 * t;
+        in.ix[t] = valid && s < k ? a.idx32[grow * k + s] : -1;
+      }
+    };
+    PassIn nxt;
+    if (!PAIR && r_beg + kFinTile * wave < r_end) load_pass(r_beg + kFinTile * wave, 0, nxt);
+  // PAIR: the tile's inputs, loaded one tile ahead
+  struct TileIn {
     uint4 qv[2 * NB];
     int qe[NB];
     int ix[KS];
   };
-  auto load_pass = [&](int r0, int pass, PassIn& in) {
-    const int r = r0 + 4 * pass + gi;
+  const int pr = lane >> 1, ph = lane & 1;  // PAIR: the lane's row within the tile, its half
+  auto load_tile = [&](int r0, TileIn& in) {
+    const int r = r0 + pr;
     const bool valid = r < r_end;
     const int64_t grow = (int64_t)bh * a.N + (valid ? r : r_beg);
     const int8_t* qsrc = a.qc + grow * a.dpad;
@@ -125,20 +162,18 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
     }
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
-      const int s = gl + 16 * t;
-      in.ix[t] = valid && s < k ? a.idx32[grow * k + s] : -1;
+      const int sl = ph + 2 * t;
+      in.ix[t] = valid && sl < k ? a.idx32[grow * k + sl] : -1;
     }
   };
-  PassIn nxt;
-  if (r_beg + kFinTile * wave < r_end) load_pass(r_beg + kFinTile * wave, 0, nxt);
+  TileIn tnxt;
+  if (PAIR && r_beg + kFinTile * wave < r_end) load_tile(r_beg + kFinTile * wave, tnxt);
   for (int r0 = r_beg + kFinTile * wave; r0 < r_end; r0 += kFinTile * a.waves) {
-    // ---- 1. kept scores, softmax, MX(P) into the code tile: four rows per pass ----
-    for (int pass = 0; pass < kFinTile / 4; ++pass) {
-      const PassIn cur = nxt;
-      if (pass + 1 < kFinTile / 4) load_pass(r0, pass + 1, nxt);
-      else if (r0 + kFinTile * a.waves < r_end) load_pass(r0 + kFinTile * a.waves, 0, nxt);
-      const int tr = 4 * pass + gi;  // row within the tile
-      const int r = r0 + tr;
+    if constexpr (PAIR) {
+      // ---- 1. kept scores, softmax, MX(P) of the tile's 32 rows: two lanes per row ----
+      const TileIn cur = tnxt;
+      if (r0 + kFinTile * a.waves < r_end) load_tile(r0 + kFinTile * a.waves, tnxt);
+      const int r = r0 + pr;
       const bool valid = r < r_end;
       const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
       const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
@@ -150,64 +185,133 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
         return t;
       };
       if (a.true_out && valid)  // debug output: every key's true score
-        for (int j = gl; j < T; j += 16) a.true_out[grow * T + j] = true_of(j);
-
-      int ix[KS];
+        for (int j = ph; j < T; j += 2) a.true_out[grow * T + j] = true_of(j);
       float v[KS];
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        ix[t] = cur.ix[t];
-        v[t] = ix[t] >= 0 ? true_of(ix[t]) : -INFINITY;
+        v[t] = cur.ix[t] >= 0 ? true_of(cur.ix[t]) : -INFINITY;
         mx = fmaxf(mx, v[t]);
       }
-      mx = __uint_as_float(row16_reduce(__float_as_uint(mx), [](uint32_t x, uint32_t y) {
-        return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
-      }));
+      mx = fmaxf(mx, __uint_as_float(dpp_u32<0xB1>(__float_as_uint(mx))));
       float sum = 0.0f;
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        v[t] = ix[t] >= 0 ? expf(v[t] - mx) : 0.0f;
+        v[t] = cur.ix[t] >= 0 ? expf(v[t] - mx) : 0.0f;
         sum += v[t];
       }
-      sum = __uint_as_float(row16_reduce(__float_as_uint(sum), [](uint32_t x, uint32_t y) {
-        return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
-      }));
-    // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
+      sum = sum + __uint_as_float(dpp_u32<0xB1>(__float_as_uint(sum)));
+      // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        if (ix[t] >= 0) {
+        if (cur.ix[t] >= 0) {
           v[t] = round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1);
-          atomicMax(&bm[ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
+          atomicMax(&bm[cur.ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
         }
       }
       wave_lds_sync();
-      if (gl < ntb) {  // block gl: scale exponent (+1024; 0 = NaN block) and flush flag
+      for (int bk = ph; bk < ntb; bk += 2) {  // block bk: scale exponent (+1024; 0 = NaN block), flush flag
         int e_raw;
-        const int es = scale_exponent(bm[gl], 127, &e_raw);
+        const int es = scale_exponent(bm[bk], 127, &e_raw);
         const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
-        sP[gl * kFinTile + tr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
-        bm[gl] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
+        sP[bk * kFinTile + pr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
+        bm[bk] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
       }
       wave_lds_sync();
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
-        if (ix[t] >= 0) {
-          const uint32_t e = bm[ix[t] >> 5];
+        if (cur.ix[t] >= 0) {
+          const uint32_t e = bm[cur.ix[t] >> 5];
           int code = 0;
           if (e & 0xFFFFu) {
             const int es = (int)(e & 0xFFFFu) - 1024;
             const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
             code = (int)round_code(x, es, 8, kRoundNearest);
           }
-          ptile[tr * vst + ix[t]] = (int8_t)code;
+          ptile[pr * vst + cur.ix[t]] = (int8_t)code;
         }
       }
       wave_lds_sync();
-      bm[gl] = 0u;
+      for (int bk = ph; bk < ntb; bk += 2) bm[bk] = 0u;
+      wave_lds_sync();
+    } else {
+    // ---- 1. kept scores, softmax, MX(P) into the code tile: four rows per pass ----
+      for (int pass = 0; pass < kFinTile / 4; ++pass) {
+        const PassIn cur = nxt;
+        if (pass + 1 < kFinTile / 4) load_pass(r0, pass + 1, nxt);
+        else if (r0 + kFinTile * a.waves < r_end) load_pass(r0 + kFinTile * a.waves, 0, nxt);
+        const int tr = 4 * pass + gi;  // row within the tile
+        const int r = r0 + tr;
+        const bool valid = r < r_end;
+        const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
+        const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
+        auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
+          bool nan = false;
+          const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
+          float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
+          if (brow) t = t + brow[(int64_t)j * a.bs3];
+          return t;
+        };
+        if (a.true_out && valid)  // debug output: every key's true score
+          for (int j = gl; j < T; j += 16) a.true_out[grow * T + j] = true_of(j);
+  
+        int ix[KS];
+        float v[KS];
+        float mx = -INFINITY;
+  #pragma unroll
+        for (int t = 0; t < KS; ++t) {
+          ix[t] = cur.ix[t];
+          v[t] = ix[t] >= 0 ? true_of(ix[t]) : -INFINITY;
+          mx = fmaxf(mx, v[t]);
+        }
+        mx = __uint_as_float(row16_reduce(__float_as_uint(mx), [](uint32_t x, uint32_t y) {
+          return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
+        }));
+        float sum = 0.0f;
+  #pragma unroll
+        for (int t = 0; t < KS; ++t) {
+          v[t] = ix[t] >= 0 ? expf(v[t] - mx) : 0.0f;
+          sum += v[t];
+        }
+        sum = __uint_as_float(row16_reduce(__float_as_uint(sum), [](uint32_t x, uint32_t y) {
+          return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
+        }));
+      // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
+  #pragma unroll
+        for (int t = 0; t < KS; ++t) {
+          if (ix[t] >= 0) {
+            v[t] = round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1);
+            atomicMax(&bm[ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
+          }
+        }
+        wave_lds_sync();
+        if (gl < ntb) {  // block gl: scale exponent (+1024; 0 = NaN block) and flush flag
+          int e_raw;
+          const int es = scale_exponent(bm[gl], 127, &e_raw);
+          const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
+          sP[gl * kFinTile + tr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
+          bm[gl] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
+        }
+        wave_lds_sync();
+  #pragma unroll
+        for (int t = 0; t < KS; ++t) {
+          if (ix[t] >= 0) {
+            const uint32_t e = bm[ix[t] >> 5];
+            int code = 0;
+            if (e & 0xFFFFu) {
+              const int es = (int)(e & 0xFFFFu) - 1024;
+              const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
+              code = (int)round_code(x, es, 8, kRoundNearest);
+            }
+            ptile[tr * vst + ix[t]] = (int8_t)code;
+          }
+        }
+        wave_lds_sync();
+        bm[gl] = 0u;
+      }
+      wave_lds_sync();
+  
     }
-    wave_lds_sync();
-
     // ---- 2. P.V on int8 MFMA: one v_mfma_i32_32x32x32_i8 per (32 columns, key block) ----
     // lane maps (checked on hardware by mxa_selftest_mfma32): A[m][k], m = lane % 32,
     // k = 16 (lane / 32) + 0..15; B[k][n], n = lane % 32, the same k; C[m][n] in c[i],
