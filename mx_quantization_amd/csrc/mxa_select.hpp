@@ -20,6 +20,7 @@
 //   workloads/deit/scripts/main.py:101-123, workloads/DiT/models.py:168-194,
 //   workloads/PixArt/models/MX_transformer_block.py:656-678, :805-825.
 #pragma once
+#include <type_traits>
 #include "mxa_topk_grp.hpp"
 
 namespace mxa {
@@ -61,6 +62,39 @@ __device__ __forceinline__ int dot32(const uint4& a0, const uint4& a1, const uin
   I = __builtin_amdgcn_sdot4((int)a1.z, (int)b1.z, I, false);
   I = __builtin_amdgcn_sdot4((int)a1.w, (int)b1.w, I, false);
   return I;
+}
+
+// ex_pred score of one key: sum_b m_b 2^(eq_b + ek_b), m_b = n_b - 2 popc(sq_b ^ sk_b)
+// (|m_b| <= 32).  When the block exponents span <= 23 bits and the smallest is >= -100,
+// the sum shifted to the smallest exponent is an exact int32, so one conversion (round
+// to nearest even) and an exact scaling give the correctly rounded float; otherwise
+// (and for NaN blocks) the exact fp64 sum.  Both equal fl32 of the exact sum.
+template <int NBD>
+__device__ __forceinline__ float expred_score(const uint32_t* sq, const int* eq, const int16_t* kex, const uint32_t* ksg,
+                                              int D) {
+  int m[NBD], e[NBD];
+  bool nan = false;
+  int emin = 1 << 20, emax = -(1 << 20);
+#pragma unroll
+  for (int b = 0; b < NBD; ++b) {
+    const int ek = exp_from16(kex[b]);
+    nan = nan || ek == kExpNaN || eq[b] == kExpNaN;
+    e[b] = eq[b] + ek;
+    m[b] = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ ksg[b]);
+    emin = min(emin, e[b]);
+    emax = max(emax, e[b]);
+  }
+  if (nan) return __uint_as_float(0x7FC00000u);
+  if (emax - emin <= 23 && emin >= -100) {
+    int sum = 0;
+#pragma unroll
+    for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
+    return ldexpf((float)sum, emin);
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int b = 0; b < NBD; ++b) acc += (double)m[b] * pow2d(e[b]);
+  return (float)acc;
 }
 
 // MX dot product of a query row (codes in registers, two uint4 per 32-block, block
@@ -200,19 +234,15 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
           sq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
           eq[b] = b < nbd ? exp_from16(a.qsA[grow * nbd + b]) : 0;
         }
-        for (int j = gl; j < T; j += 16) {
-          double acc = 0.0;
-          bool nan = false;
-#pragma unroll
-          for (int b = 0; b < kMaxNB; ++b) {
-            if (b < nbd) {
-              const int e = exp_from16(tex[j * nbd + b]);
-              nan = nan || e == kExpNaN || eq[b] == kExpNaN;
-              const int m = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ tsg[j * nbd + b]);
-              acc += (double)m * pow2d(nan ? 0 : eq[b] + e);
-            }
-          }
-          emit(j, nan ? __uint_as_float(0x7FC00000u) : (float)acc);
+        auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
+          constexpr int NBD = decltype(nbd_c)::value;
+          for (int j = gl; j < T; j += 16) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
+        };
+        switch (nbd) {
+          case 1: keys(std::integral_constant<int, 1>{}); break;
+          case 2: keys(std::integral_constant<int, 2>{}); break;
+          case 3: keys(std::integral_constant<int, 3>{}); break;
+          default: keys(std::integral_constant<int, 4>{}); break;
         }
       } else if constexpr (MODE == kModeElsa) {
         // approx = ||MX_K[row r]|| * cos(clamp(pi/D * hamming - 0.127, 0))
