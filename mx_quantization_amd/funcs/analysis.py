@@ -49,14 +49,17 @@ def init_analysis_files(attn_type, anal_dir, k, approx_flag, pred_mode, total_ti
 
 
 def total_chosen_k(pred_idx):
-    """Mean over (batch, head) of |unique chosen keys| / rows (analysis.py:56-110)."""
+    """Mean over (batch, head) of |unique chosen keys| / rows (analysis.py:56-110),
+    vectorised on idx's device: the union of the rows' prune masks per (batch, head)
+    (scatter), its popcount, instead of a torch.unique per head."""
     B, H = pred_idx.shape[0], pred_idx.shape[1]
     rows = pred_idx.shape[-2]
-    total = 0.0
-    for b in range(B):
-        for h in range(H):
-            total += torch.unique(pred_idx[b, h].flatten()).numel() / rows
-    return total / (B * H)
+    flat = pred_idx.reshape(B, H, -1).long()
+    T = int(flat.max().item()) + 1 if flat.numel() else 1
+    union = torch.zeros((B, H, T), dtype=torch.bool, device=pred_idx.device)
+    union.scatter_(-1, flat, True)
+    cov = union.sum(dim=-1).to(torch.float64) / rows
+    return float(cov.mean().item())
 
 
 def diff_idx_analysis(true_idx: torch.Tensor, pred_idx: torch.Tensor):

@@ -231,6 +231,25 @@ def gen_linear_qkv():
     print("wrote linear_qkv")
 
 
+def gen_analysis():
+    """analysis.npz: the reference's funcs/analysis.py hooks (total_chosen_k :56-110,
+    diff_idx_analysis :136-157, save_idx_file :22-29) on seeded top-k outputs."""
+    import tempfile
+    from funcs import total_chosen_k, diff_idx_analysis, save_idx_file
+    g = torch.Generator().manual_seed(5)
+    idx = torch.randint(0, 197, (3, 4, 197, 20), generator=g)
+    true_vals = torch.rand((120, 2, 8, 20), generator=g)
+    scores = torch.where(torch.rand((120, 2, 8, 20), generator=g) < 0.7, true_vals, torch.rand((120, 2, 8, 20), generator=g))
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "idx.txt")
+        save_idx_file(idx[:, :, :5, :], f, block_idx=3)
+        text = open(f).read()
+    np.savez_compressed(os.path.join(OUT, "analysis.npz"), idx=idx.numpy(), true_vals=true_vals.numpy(),
+                        scores=scores.numpy(), chosen_k=np.float64(total_chosen_k(idx)),
+                        diff=np.float64(diff_idx_analysis(true_vals, scores)), idx_text=np.array(text))
+    print("wrote analysis")
+
+
 def gen_quant_kat():
     """Known-answer + boundary vectors through the reference's _quantize_mx."""
     out = {}
@@ -352,6 +371,6 @@ def gen_topk_ties():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv"]
+    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv", "analysis"]
     for w in which:
         globals()["gen_" + w]()

@@ -2,6 +2,8 @@
 symbol include/mxa.h declares, the Python surfaces import under the reference's
 names, and the product path refuses CPU tensors (no fallback)."""
 import os
+
+import numpy as np
 import re
 
 import pytest
@@ -123,3 +125,20 @@ def test_attention_path_selection_is_host_logic():
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 3, 197, 197, 64, 20, top_k=0))) == fused
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 600, 64, 5))) == -2  # T > 512
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 60, 160, 5))) == -2  # D > 128
+
+
+def test_analysis_hooks_vs_reference():
+    """The drop-in funcs/analysis.py hooks against the reference's own outputs
+    (tests/golden/analysis.npz from gen_golden.py): total_chosen_k, diff_idx_analysis,
+    save_idx_file's text."""
+    import tempfile
+    from mx_quantization_amd.funcs import analysis as A
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "analysis.npz"))
+    idx = torch.from_numpy(d["idx"])
+    assert A.total_chosen_k(idx) == pytest.approx(float(d["chosen_k"]), rel=1e-12)
+    assert A.diff_idx_analysis(torch.from_numpy(d["true_vals"]), torch.from_numpy(d["scores"])) == \
+        pytest.approx(float(d["diff"]), rel=1e-6)
+    with tempfile.TemporaryDirectory() as t:
+        f = os.path.join(t, "idx.txt")
+        A.save_idx_file(idx[:, :, :5, :], f, block_idx=3)
+        assert open(f).read() == str(d["idx_text"])
