@@ -224,17 +224,17 @@ static int launch_dense_s(const Rows2Args& ra0, int BH, hipStream_t stream, bool
 }
 
 // ---- selection kernel (mxa_select.hpp): four query rows per wave -------------------
-template <int NP, int MODE>
+template <int NP, int MODE, int W>
 static size_t select_lds(const Rows2Args& ra) {
-  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * kSelWaves * grp_row_bytes(grp_alloc(ra.T), NP);
+  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP);
 }
-template <int NP, int MODE>
-static int launch_select_np(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
+template <int NP, int MODE, int W>
+static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
   Rows2Args ra = ra0;
-  const size_t lds = select_lds<NP, MODE>(ra);
+  const size_t lds = select_lds<NP, MODE, W>(ra);
   if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   if (plan) return MXA_OK;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
@@ -242,8 +242,13 @@ static int launch_select_np(const Rows2Args& ra0, int BH, hipStream_t stream, bo
   while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
   ra.rows_per_wg = rows;
   const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_kernel<NP, MODE>), dim3((unsigned)BH, gy), dim3(64 * kSelWaves), lds, stream, ra);
+  hipLaunchKernelGGL((select_kernel<NP, MODE, W>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NP, int MODE>
+static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
+  return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
 }
 template <int MODE>
 static int launch_select_m(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {

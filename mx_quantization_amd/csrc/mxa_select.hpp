@@ -25,8 +25,22 @@
 
 namespace mxa {
 
-constexpr int kSelWaves = 4;  // waves per workgroup
-constexpr int kSelRows = 32;  // query rows per workgroup (a multiple of 4 * kSelWaves)
+#ifndef MXA_SEL_ROWS  // tools builds vary these (build_native defines)
+#define MXA_SEL_ROWS 32
+#endif
+#ifndef MXA_SEL_OCC
+#define MXA_SEL_OCC 4
+#endif
+#ifndef MXA_SEL_SHORT_T
+#define MXA_SEL_SHORT_T 224
+#endif
+constexpr int kSelRows = MXA_SEL_ROWS;  // query rows per workgroup (a multiple of 4 * waves)
+// waves per workgroup: 2 for rows of <= 224 keys on a large grid (DeiT-base: 0.97 ->
+// 0.93 ms), else 4 (DiT: 1.44 vs 1.56 ms with 2; PixArt's 128 heads: 0.069 vs 0.10 ms)
+// -- measured, tools/bench_cmp.sh
+inline int sel_waves_for(int T, int64_t BH, int N) {
+  return T <= MXA_SEL_SHORT_T && BH * ((N + kSelRows - 1) / kSelRows) >= 8192 ? 2 : 4;
+}
 
 // LDS layout of the score tables (then the per-row top-k areas)
 struct SelLds {
@@ -159,8 +173,8 @@ __device__ __forceinline__ float elsa_cos_entry(int D, int h) {
   return (float)cos((double)cor);
 }
 
-template <int NP, int MODE>
-__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void select_kernel(Rows2Args a) {
+template <int NP, int MODE, int kSelWaves>
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
