@@ -23,8 +23,7 @@
 // window that holds every pending range of the wave), so a step costs ~E
 // instructions per lane for FOUR rows at once instead of ~100+ per row for a
 // wave-wide step.  The row itself lives in an LDS mirror A (order key << 32 | index);
-// swaps publish their positions in P and then write their element to the partner's
-// position.
+// swaps publish their positions in P, then the pairs trade elements.
 //
 // std::sort's final insertion sort is a stable sort of the arrangement the introsort
 // loop leaves; because those segments are mutually ordered it equals a stable sort of
@@ -120,7 +119,7 @@ constexpr int pow2_floor() { return E >= 32 ? 32 : E >= 16 ? 16 : E >= 8 ? 8 : E
 // (f+1, mid, l-1) moved to f, then __unguarded_partition of (f, l)) on every row of
 // the wave with act set (l - f >= 4), all rows in lockstep.  Window: lane gl holds
 // positions lb + e, lb = b + E*gl, e < E (b even, b <= f, l <= b + 16E <= NPA).
-// HP = NP / 2 (> any swap count).  Returns the cut.
+// HP = NP / 2 (>= any swap count).  Returns the cut.
 template <int E, int NP>
 __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
   constexpr int HP = NP / 2;
@@ -175,42 +174,32 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
     j = ok ? c : j;
   }
   const int cut = b + (int)g_sum((uint32_t)j);
-  // swapping left stops: the left stops below the cut (nsw of them); swapping right
-  // stops: the nsw highest, i.e. this lane's right stops after its first j0
+  // swapping left stops: the left stops below the cut (nsw of them, left ranks
+  // 0 .. nsw-1); swapping right stops: the nsw highest (ranks from the top 0 .. nsw-1)
   const int cl = min(max(cut - lb, 0), E);
   const uint32_t SLm = Lm & ~lowbits(E - cl);
   const uint32_t nsw = g_sum((uint32_t)__popc(SLm));
-  const int j0 = min(max((int)(totR - nsw) - (int)PR, 0), E);
-  int c0 = 0;  // the longest prefix with fewer than j0 right stops: it ends at the j0-th
-#pragma unroll
-  for (int st = pow2_floor<E>(); st >= 1; st >>= 1) {
-    const int c = c0 + st, sh = c <= E ? E - c : 0;
-    const bool ok = c <= E && (int)__popc(Rm >> sh) < j0;
-    c0 = ok ? c : c0;
-  }
-  const int p0 = j0 == 0 ? 0 : min(c0 + 1, E);
-  const uint32_t SRm = Rm & lowbits(E - p0);
-  const uint32_t SW = SLm | SRm;
-  // the exchange: every swapping stop publishes its position in its slot (left: its
-  // rank among left stops; right: HP + its rank from the top); then each writes its
-  // element to the partner's position.  Non-swapping positions use the lane's trash
-  // slot and rewrite their own element (no exec-mask branches).
+  // the exchange: every swapping left stop publishes its position at HP + its rank,
+  // every swapping right stop at its rank from the top, the rest at the lane's trash
+  // slot; then the t-th pairs trade elements, 16 pairs a row at a time (only the
+  // swaps move: ~range/4 of the positions)
   const uint32_t trash = 2 * HP + gl;
-  uint32_t slot[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int sh = E - 1 - e;
-    const uint32_t tl = PL + (uint32_t)__popc((Lm >> sh) >> 1);
-    const uint32_t tr = (uint32_t)HP + totR - PR - (uint32_t)__popc(Rm >> sh);
-    slot[e] = ((SW >> sh) & 1u) ? (((SLm >> sh) & 1u) ? tl : tr) : trash;
-    p_put<NP>(g, slot[e], (uint32_t)(lb + e));
+    const uint32_t tl = HP + PL + (uint32_t)__popc((Lm >> sh) >> 1);
+    const uint32_t tr = totR - PR - (uint32_t)__popc(Rm >> sh);
+    const uint32_t slot = ((SLm >> sh) & 1u) ? tl : (((Rm >> sh) & 1u) && tr < nsw ? tr : trash);
+    p_put<NP>(g, slot, (uint32_t)(lb + e));
   }
   wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const bool sw = (SW >> (E - 1 - e)) & 1u;
-    const uint32_t q = p_get<NP>(g, sw ? slot[e] ^ (uint32_t)HP : slot[e]);
-    g.A[sw ? (int)q : lb + e] = pack_ki(K[e], I[e]);
+  for (uint32_t t = gl; __builtin_amdgcn_ballot_w64(t < nsw) != 0; t += 16) {
+    if (t < nsw) {
+      const uint32_t y = p_get<NP>(g, t), x = p_get<NP>(g, HP + t);
+      const uint64_t ax = g.A[x], ay = g.A[y];
+      g.A[x] = ay;
+      g.A[y] = ax;
+    }
   }
   wave_lds_sync();
   return cut;
