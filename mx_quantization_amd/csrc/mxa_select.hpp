@@ -250,7 +250,50 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
         }
         auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
           constexpr int NBD = decltype(nbd_c)::value;
-          for (int j = gl; j < T; j += 16) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
+          if (brow) {
+            for (int j = gl; j < T; j += 16) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
+            return;
+          }
+          // no bias: the raw int16 exponents (NaN = INT16_MIN) go straight into the
+          // fast-path test -- a NaN block drives the smallest exponent below -100 --
+          // and a fast-path value (finite, never -0) takes the three-instruction key
+          int eqr[NBD], nbk[NBD];
+#pragma unroll
+          for (int b = 0; b < NBD; ++b) {
+            eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
+            nbk[b] = min(32, D - 32 * b);
+          }
+          for (int j = gl; j < T; j += 16) {
+            const int16_t* kex = tex + j * NBD;
+            const uint32_t* ksg = tsg + j * NBD;
+            int e[NBD], m[NBD];
+#pragma unroll
+            for (int b = 0; b < NBD; ++b) {
+              e[b] = eqr[b] + (int)kex[b];
+              m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
+            }
+            int emin = e[0], emax = e[0];
+#pragma unroll
+            for (int b = 1; b < NBD; ++b) {
+              emin = min(emin, e[b]);
+              emax = max(emax, e[b]);
+            }
+            float v;
+            uint32_t key;
+            if (emax - emin <= 23 && emin >= -100) {
+              int sum = 0;
+#pragma unroll
+              for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
+              v = ldexpf((float)sum, emin);
+              const uint32_t u = __float_as_uint(v);
+              key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
+            } else {
+              v = expred_score<NBD>(sq, eq, kex, ksg, D);
+              key = order_key(v);
+            }
+            if (a.pred_out) a.pred_out[grow * T + j] = v;
+            g.A[j] = pack_ki(key, (uint32_t)j);
+          }
         };
         switch (nbd) {
           case 1: keys(std::integral_constant<int, 1>{}); break;

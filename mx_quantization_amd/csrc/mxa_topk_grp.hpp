@@ -183,14 +183,18 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // every swapping right stop at its rank from the top, the rest at the lane's trash
   // slot; then the t-th pairs trade elements, 16 pairs a row at a time (only the
   // swaps move: ~range/4 of the positions)
-  const uint32_t trash = 2 * HP + gl;
+  // (u8 slots: the slot values are LDS byte addresses, the base folded into the
+  // popcount accumulations)
+  const uint32_t ob = NP <= 256 ? (uint32_t)(size_t)g.P : 0u;
+  const uint32_t trash = ob + 2 * HP + gl, lbase = ob + HP + PL, rbase = ob + totR - PR, rlim = ob + nsw;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int sh = E - 1 - e;
-    const uint32_t tl = HP + PL + (uint32_t)__popc((Lm >> sh) >> 1);
-    const uint32_t tr = totR - PR - (uint32_t)__popc(Rm >> sh);
-    const uint32_t slot = ((SLm >> sh) & 1u) ? tl : (((Rm >> sh) & 1u) && tr < nsw ? tr : trash);
-    p_put<NP>(g, slot, (uint32_t)(lb + e));
+    const uint32_t tl = lbase + (uint32_t)__popc((Lm >> sh) >> 1);
+    const uint32_t tr = rbase - (uint32_t)__popc(Rm >> sh);
+    const uint32_t slot = ((SLm >> sh) & 1u) ? tl : (((Rm >> sh) & 1u) && tr < rlim ? tr : trash);
+    if constexpr (NP <= 256) *(lu8*)(size_t)slot = (uint8_t)(lb + e);
+    else p_put<NP>(g, slot, (uint32_t)(lb + e));
   }
   wave_lds_sync();
   for (uint32_t t = gl; __builtin_amdgcn_ballot_w64(t < nsw) != 0; t += 16) {
