@@ -124,14 +124,13 @@ template <int E, int NP>
 __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
   constexpr int HP = NP / 2;
   const int fa = act ? f : 0, la = act ? l : 4;  // idle rows read harmless positions
-  const int mid = fa + (la - fa) / 2;
-  const uint64_t xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1], xf = g.A[fa];
-  const uint32_t ka = hi32(xa), kb = hi32(xb), kc = hi32(xc);
+  const int mid = fa + (int)((uint32_t)(la - fa) >> 1);
+  const lu32* A32 = (const lu32*)g.A;  // the keys alone (32-bit compares)
+  const uint32_t ka = A32[2 * fa + 3], kb = A32[2 * mid + 1], kc = A32[2 * la - 1];
   // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free
   const bool ab = ka > kb, bc = kb > kc, ac = ka > kc;
-  const int sel = ab ? (bc ? 1 : (ac ? 2 : 0)) : (ac ? 0 : (bc ? 2 : 1));
-  const int m = sel == 0 ? fa + 1 : (sel == 1 ? mid : la - 1);
-  const uint64_t xm = sel == 0 ? xa : (sel == 1 ? xb : xc);
+  const int m = ab ? (bc ? mid : (ac ? la - 1 : fa + 1)) : (ac ? fa + 1 : (bc ? la - 1 : mid));
+  const uint64_t xm = g.A[m], xf = g.A[fa];
   const uint32_t p = hi32(xm);
   if (act) {  // iter_swap(f, median)
     g.A[f] = xm;
