@@ -91,6 +91,19 @@ __device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd)
   return y < 0.0f ? -r : r;
 }
 
+// The MXINT8 nearest-rounding case of round_code as an int: x * 2^(6-es) is exact and
+// equals (x * 2^-es) * 64, so one multiply by q8_scale(es) does, except for es < -121
+// where 2^(6-es) is no float (then q8_scale = 2^-es and TINY multiplies by 64 after);
+// the sign goes back on with a bit copy (-0 converts to 0 like +0).
+__device__ __forceinline__ float q8_scale(int es) { return pow2f(es >= -121 ? 6 - es : -es); }
+template <bool TINY>
+__device__ __forceinline__ int q8_code(float x, float s) {
+  float y = x * s;
+  if (TINY) y = y * 64.0f;
+  const float r = fminf(floorf(fabsf(y) + 0.5f), 127.0f);
+  return (int)__builtin_copysignf(r, y);
+}
+
 // bfloatX element quantization, exp_bits = 8, mbits = bfloat-7 (elemwise_ops.py:201-216
 // -> _quantize_elemwise_core :92-180 with saturate_normals=False).  bfloat in {0,32} = identity.
 __device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int allow_denorm) {

@@ -1,6 +1,7 @@
 // Per-block bodies of the attention operand builders, shared by the standalone
 // prep kernels (mxa_quant.hip) and the fused qkv projection (mxa_proj.hpp).
 #pragma once
+#include <type_traits>
 #include "mxa_kernels.hpp"
 
 namespace mxa {
@@ -144,6 +145,74 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
   }
 }
 
+// rows_prep_block for the plain case -- no bfloat rounding, no subnormal flush, no
+// true_ex zero indicators, approximator operand the sign (ex_pred) or the MXINT8 code --
+// with the int8 code path of q8_code: the same outputs in about a third of the VALU
+// (the prep launch is VALU-bound next to its HBM stream otherwise)
+__device__ __forceinline__ bool rows_prep_plain(const RowsPrepArgs& a) {
+  return (a.bfloat == 0 || a.bfloat == 32) && !a.flush && !a.zind &&
+         (a.op_kind == MXA_OP_MXINT8 || (a.op_kind == MXA_OP_SIGN && !a.op));
+}
+template <int EPL>
+__device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int64_t row, int blk, int sub, int c0,
+                                                      const float xv[EPL], bool valid) {
+  constexpr int LPB = 32 / EPL;
+  uint32_t mb = 0;
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) mb = max(mb, __float_as_uint(xv[j]) & 0x7FFFFFFFu);
+  mb = blk_reduce<LPB>(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  int e_raw;
+  const int es = scale_exponent(mb, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  int code[EPL];
+  auto quant = [&](auto tiny) {
+    const float s = q8_scale(es);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) code[j] = q8_code<decltype(tiny)::value>(xv[j], s);
+  };
+  if (nanblk) {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) code[j] = 0;
+  } else if (es >= -121) {
+    quant(std::false_type{});
+  } else {
+    quant(std::true_type{});
+  }
+  int maxc = 0;
+  uint32_t sw = 0u;
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) {
+    maxc = max(maxc, abs(code[j]));
+    sw |= (code[j] < 0 ? 1u : 0u) << (EPL * sub + j);
+  }
+  maxc = (int)blk_reduce<LPB>((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+  sw = blk_reduce<LPB>(sw, [](uint32_t u, uint32_t w) { return u | w; });
+  if (valid) {
+    uint32_t pc[EPL / 4];
+#pragma unroll
+    for (int w = 0; w < EPL / 4; ++w)
+      pc[w] = (uint32_t)(code[4 * w] & 0xFF) | (uint32_t)(code[4 * w + 1] & 0xFF) << 8 |
+              (uint32_t)(code[4 * w + 2] & 0xFF) << 16 | (uint32_t)code[4 * w + 3] << 24;
+    const int64_t base = row * a.dpad + c0;
+    if constexpr (EPL == 16) {
+      const uint4 v = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+      if (a.codes) *reinterpret_cast<uint4*>(a.codes + base) = v;
+      if (a.op) *reinterpret_cast<uint4*>(a.op + base) = v;  // MXA_OP_MXINT8 (SIGN has none)
+    } else {
+      if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc[0];
+      if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = pc[0];
+    }
+    if (sub == 0) {
+      // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
+      // floor(log2(maxc * 2^(es-6))) = floor(log2 maxc) + es - 6 exactly (maxc <= 127)
+      const int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : 31 - __clz(maxc) + es - 6);
+      if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
+      if (a.sA) a.sA[row * a.nb + blk] = exp_to16(a.op_kind == MXA_OP_SIGN ? eA : (nanblk ? kExpNaN : es - 6));
+      if (a.signs) a.signs[row * a.nb + blk] = sw;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // operand builder for matrices quantized along the row axis (V, and in2 of
 // mx.matmul): blocks of 32 rows per column; output transposed [col][row] codes.
@@ -159,17 +228,33 @@ __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t 
   const bool nanblk = es == kExpNaN;
   const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
   uint32_t w[8];
+  if (!flush && !nanblk && a.mbits == 8) {  // the plain MXINT8 case: q8_code
+    const float s = q8_scale(es);
+    auto quant = [&](auto tiny) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    uint32_t acc = 0;
+      for (int q = 0; q < 8; ++q) {
+        int cd[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = xv[q * 4 + j];
-      if (flush) v = v * 0.0f;
-      const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest);
-      acc |= (uint32_t)(cd & 0xFF) << (8 * j);
+        for (int j = 0; j < 4; ++j) cd[j] = q8_code<decltype(tiny)::value>(xv[q * 4 + j], s);
+        w[q] = (uint32_t)(cd[0] & 0xFF) | (uint32_t)(cd[1] & 0xFF) << 8 | (uint32_t)(cd[2] & 0xFF) << 16 |
+               (uint32_t)cd[3] << 24;
+      }
+    };
+    if (es >= -121) quant(std::false_type{});
+    else quant(std::true_type{});
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = xv[q * 4 + j];
+        if (flush) v = v * 0.0f;
+        const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest);
+        acc |= (uint32_t)(cd & 0xFF) << (8 * j);
+      }
+      w[q] = acc;
     }
-    w[q] = acc;
   }
   int8_t* dst = a.codes_t + (m * a.C + c) * a.rpad + r0;
   uint4* d4 = reinterpret_cast<uint4*>(dst);

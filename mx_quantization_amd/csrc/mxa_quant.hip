@@ -145,7 +145,8 @@ __device__ __forceinline__ void rows_prep_body(const RowsPrepArgs& a, uint32_t b
 #pragma unroll
     for (int j = 0; j < 16; ++j) xv[j] = (valid && c0 + j < a.D) ? xr[c0 + j] : 0.0f;
   }
-  rows_prep_block<16>(a, row, blk, sub, c0, xv, valid);
+  if (rows_prep_plain(a)) rows_prep_block_plain<16>(a, row, blk, sub, c0, xv, valid);
+  else rows_prep_block<16>(a, row, blk, sub, c0, xv, valid);
 }
 __global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) { rows_prep_body(a, blockIdx.x); }
 
