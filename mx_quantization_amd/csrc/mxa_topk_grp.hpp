@@ -94,6 +94,22 @@ __device__ __forceinline__ uint32_t g_shl_le(uint32_t acc, uint32_t a, uint32_t 
   return acc;
 }
 
+// r + (a > b) for 64-bit a, b: a compare and an add-with-carry
+__device__ __forceinline__ uint32_t g_add_gt(uint32_t r, uint64_t a, uint64_t b) {
+  asm("v_cmp_gt_u64 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, 0, vcc" : "+v"(r) : "v"(a), "v"(b) : "vcc");
+  return r;
+}
+// ri += (cj > ci), rj -= (cj > ci): one 64-bit compare, an add-with-carry and a
+// subtract-with-borrow (left to itself the compiler keeps every compare mask live and
+// sums them at the end)
+__device__ __forceinline__ void g_pair_rank(uint32_t& ri, uint32_t& rj, uint64_t cj, uint64_t ci) {
+  uint64_t t;
+  asm("v_cmp_gt_u64 vcc, %3, %4\n\tv_addc_co_u32_e64 %0, %2, %0, 0, vcc\n\tv_subb_co_u32_e64 %1, %2, %1, 0, vcc"
+      : "+v"(ri), "+v"(rj), "=&s"(t)
+      : "v"(cj), "v"(ci)
+      : "vcc");
+}
+
 // DPP within each 16-lane row: row_shr with zero fill, row_newbcast:15
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
@@ -246,10 +262,15 @@ __device__ __forceinline__ void grp_rank_prefix(const GrpRow& g, int m, bool val
     K[e + 1] = v.w;
     r[e] = r[e + 1] = 0u;
   }
-  for (int w = 0; w < m; ++w) {
-    const uint32_t kw = hi32(g.A[w]);
+  // composites (key << 32 | 0xFFFF - position): unique, larger for the earlier of two
+  // equal keys, so a position's rank is the number of larger composites
+  uint64_t C[EP];
 #pragma unroll
-    for (int e = 0; e < EP; ++e) r[e] += (kw > K[e] || (kw == K[e] && w < z0 + e)) ? 1u : 0u;
+  for (int e = 0; e < EP; ++e) C[e] = ((uint64_t)K[e] << 32) | (uint32_t)(0xFFFF - (z0 + e));
+  for (int w = 0; w < m; ++w) {
+    const uint64_t cw = (g.A[w] & 0xFFFFFFFF00000000ull) | (uint32_t)(0xFFFF - w);
+#pragma unroll
+    for (int e = 0; e < EP; ++e) r[e] = g_add_gt(r[e], cw, C[e]);
   }
   wave_lds_sync();
 #pragma unroll
@@ -257,29 +278,33 @@ __device__ __forceinline__ void grp_rank_prefix(const GrpRow& g, int m, bool val
     if (valid && z0 + e < m) g.A[r[e]] = pack_ki(K[e], I[e]);
 }
 
-// stable rank of each queued segment (2..16 elements), one lane per segment
+// stable rank of each queued segment (2..16 elements), one lane per segment: element i
+// as the composite (key << 32 | 15 - i) -- unique, and larger for the earlier of two
+// equal keys -- so its rank is the number of larger composites, one 64-bit compare
+// per pair feeding both ranks
 __device__ __forceinline__ void grp_rank_segments(const GrpRow& g, int ns, int gl) {
   if (gl < ns) {
     const uint32_t sg = g.seg[gl];
     const int f = (int)(sg & 0xFFFFu), len = (int)(sg >> 16) - f;
-    uint64_t x[16];
-    uint32_t r[16];
+    uint64_t c[16];
+    uint32_t ix[16], r[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      x[i] = i < len ? (uint64_t)g.A[f + i] : 0ull;  // key 0 sorts after every real key
-      r[i] = 0u;
+      const uint64_t x = i < len ? (uint64_t)g.A[f + i] : 0ull;  // key 0 sorts after every real key
+      c[i] = (x & 0xFFFFFFFF00000000ull) | (uint32_t)(15 - i);
+      ix[i] = (uint32_t)x;
+      r[i] = (uint32_t)i;
     }
+    // r[i] starts at i (every earlier element counted as larger), drops for each
+    // earlier one that is smaller and grows for each later one that is larger
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (j < i) r[i] += hi32(x[j]) >= hi32(x[i]) ? 1u : 0u;
-        if (j > i) r[i] += hi32(x[j]) > hi32(x[i]) ? 1u : 0u;
-      }
+      for (int j = i + 1; j < 16; ++j) g_pair_rank(r[i], r[j], c[j], c[i]);
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (i < len) g.A[f + r[i]] = x[i];
+      if (i < len) g.A[f + r[i]] = (c[i] & 0xFFFFFFFF00000000ull) | ix[i];
   }
 }
 
