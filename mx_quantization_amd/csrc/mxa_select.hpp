@@ -263,6 +263,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
             eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
             nbk[b] = min(32, D - 32 * b);
           }
+          float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
           for (int j = gl; j < T; j += 16) {
             const int16_t* kex = tex + j * NBD;
             const uint32_t* ksg = tsg + j * NBD;
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
               v = expred_score<NBD>(sq, eq, kex, ksg, D);
               key = order_key(v);
             }
-            if (a.pred_out) a.pred_out[grow * T + j] = v;
+            if (prow) prow[j] = v;
             g.A[j] = pack_ki(key, (uint32_t)j);
           }
         };
