@@ -99,12 +99,12 @@ __device__ __forceinline__ uint32_t g_add_gt(uint32_t r, uint64_t a, uint64_t b)
   asm("v_cmp_gt_u64 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, 0, vcc" : "+v"(r) : "v"(a), "v"(b) : "vcc");
   return r;
 }
-// ri += (cj > ci), rj -= (cj > ci): one 64-bit compare, an add-with-carry and a
+// ri += (kj > ki), rj -= (kj > ki): one compare, an add-with-carry and a
 // subtract-with-borrow (left to itself the compiler keeps every compare mask live and
 // sums them at the end)
-__device__ __forceinline__ void g_pair_rank(uint32_t& ri, uint32_t& rj, uint64_t cj, uint64_t ci) {
+__device__ __forceinline__ void g_pair_rank(uint32_t& ri, uint32_t& rj, uint32_t cj, uint32_t ci) {
   uint64_t t;
-  asm("v_cmp_gt_u64 vcc, %3, %4\n\tv_addc_co_u32_e64 %0, %2, %0, 0, vcc\n\tv_subb_co_u32_e64 %1, %2, %1, 0, vcc"
+  asm("v_cmp_gt_u32 vcc, %3, %4\n\tv_addc_co_u32_e64 %0, %2, %0, 0, vcc\n\tv_subb_co_u32_e64 %1, %2, %1, 0, vcc"
       : "+v"(ri), "+v"(rj), "=&s"(t)
       : "v"(cj), "v"(ci)
       : "vcc");
@@ -278,33 +278,32 @@ __device__ __forceinline__ void grp_rank_prefix(const GrpRow& g, int m, bool val
     if (valid && z0 + e < m) g.A[r[e]] = pack_ki(K[e], I[e]);
 }
 
-// stable rank of each queued segment (2..16 elements), one lane per segment: element i
-// as the composite (key << 32 | 15 - i) -- unique, and larger for the earlier of two
-// equal keys -- so its rank is the number of larger composites, one 64-bit compare
-// per pair feeding both ranks
+// stable rank of each queued segment (2..16 elements), one lane per segment: the rank
+// of element i counts the later elements with a larger key and the earlier ones with a
+// larger or equal key -- r[i] starts at i and each pair (i < j) moves one count with
+// one 32-bit compare (few registers live: the elements are re-read for the moves)
 __device__ __forceinline__ void grp_rank_segments(const GrpRow& g, int ns, int gl) {
   if (gl < ns) {
     const uint32_t sg = g.seg[gl];
     const int f = (int)(sg & 0xFFFFu), len = (int)(sg >> 16) - f;
-    uint64_t c[16];
-    uint32_t ix[16], r[16];
+    const lu32* A32 = (const lu32*)g.A;
+    uint32_t kk[16], r[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const uint64_t x = i < len ? (uint64_t)g.A[f + i] : 0ull;  // key 0 sorts after every real key
-      c[i] = (x & 0xFFFFFFFF00000000ull) | (uint32_t)(15 - i);
-      ix[i] = (uint32_t)x;
+      kk[i] = i < len ? A32[2 * (f + i) + 1] : 0u;  // key 0 sorts after every real key
       r[i] = (uint32_t)i;
     }
-    // r[i] starts at i (every earlier element counted as larger), drops for each
-    // earlier one that is smaller and grows for each later one that is larger
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
-      for (int j = i + 1; j < 16; ++j) g_pair_rank(r[i], r[j], c[j], c[i]);
+      for (int j = i + 1; j < 16; ++j) g_pair_rank(r[i], r[j], kk[j], kk[i]);
     }
+    uint64_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = i < len ? (uint64_t)g.A[f + i] : 0ull;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (i < len) g.A[f + r[i]] = (c[i] & 0xFFFFFFFF00000000ull) | ix[i];
+      if (i < len) g.A[f + r[i]] = x[i];
   }
 }
 
