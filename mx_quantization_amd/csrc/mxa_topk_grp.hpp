@@ -225,25 +225,28 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
 }
 
 // one partition of [f, l) on every row with act, in the narrowest window (16 E
-// positions from an even base at or below f) that holds every acting row's range
+// positions from an even base at or below f) that holds every acting row's range.
+// The base is min(f & ~1, NPA - 16 E); a range fits iff need = l - (f & ~1) <= 16 E
+// (when the base is clamped, l <= NPA makes it fit anyway), so each candidate width
+// costs one compare of the precomputed need.
 template <int E, int NP>
-__device__ __forceinline__ bool grp_try(const GrpRow& g, int f, int l, bool act, int gl, int& cut) {
+__device__ __forceinline__ bool grp_try(const GrpRow& g, int f, int l, int need, bool act, int gl, int& cut) {
   if (16 * E > NP || 16 * E > g.npa) return false;
-  const int b = min(f & ~1, g.npa - 16 * E);
-  if (__builtin_amdgcn_ballot_w64(act && l - b > 16 * E) != 0) return false;
-  cut = grp_partition<E, NP>(g, f, l, b, act, gl);
+  if (__builtin_amdgcn_ballot_w64(need > 16 * E) != 0) return false;
+  cut = grp_partition<E, NP>(g, f, l, min(f & ~1, g.npa - 16 * E), act, gl);
   return true;
 }
 template <int NP>
 __device__ __forceinline__ int grp_partition_any(const GrpRow& g, int f, int l, bool act, int gl) {
   int cut = 0;
-  if (grp_try<2, NP>(g, f, l, act, gl, cut) || grp_try<4, NP>(g, f, l, act, gl, cut) ||
-      grp_try<6, NP>(g, f, l, act, gl, cut) || grp_try<8, NP>(g, f, l, act, gl, cut) ||
-      grp_try<10, NP>(g, f, l, act, gl, cut) || grp_try<12, NP>(g, f, l, act, gl, cut) ||
-      grp_try<14, NP>(g, f, l, act, gl, cut) || grp_try<16, NP>(g, f, l, act, gl, cut) ||
-      grp_try<24, NP>(g, f, l, act, gl, cut))
+  const int need = act ? l - (f & ~1) : 0;
+  if (grp_try<2, NP>(g, f, l, need, act, gl, cut) || grp_try<4, NP>(g, f, l, need, act, gl, cut) ||
+      grp_try<6, NP>(g, f, l, need, act, gl, cut) || grp_try<8, NP>(g, f, l, need, act, gl, cut) ||
+      grp_try<10, NP>(g, f, l, need, act, gl, cut) || grp_try<12, NP>(g, f, l, need, act, gl, cut) ||
+      grp_try<14, NP>(g, f, l, need, act, gl, cut) || grp_try<16, NP>(g, f, l, need, act, gl, cut) ||
+      grp_try<24, NP>(g, f, l, need, act, gl, cut))
     return cut;
-  grp_try<32, NP>(g, f, l, act, gl, cut);
+  if constexpr (NP >= 512) cut = grp_partition<32, NP>(g, f, l, min(f & ~1, g.npa - 512), act, gl);
   return cut;
 }
 
