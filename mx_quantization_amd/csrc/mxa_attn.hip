@@ -367,8 +367,40 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B), dim3(64 * 3 * NBD), lds,
-                     stream, pa);
+  // head groups: a workgroup loops over hpg heads after staging its x tile once; the
+  // group count minimises (rounds of resident workgroups) x (heads + ~1/4 head of x
+  // staging) -- with all heads per workgroup DeiT-base's 1,792 workgroups ran 3.5
+  // rounds of 512 resident ones, the last half empty
+  static int per_cu = -1, cus = -1;
+  static size_t lds_q = 0;  // the LDS size the occupancy was queried for
+  if (per_cu < 0 || lds_q != lds) {
+    lds_q = lds;
+    int dev = 0, n = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
+                                                     64 * 3 * NBD, lds) != hipSuccess || n < 1)
+      n = 1;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
+    per_cu = n;
+    cus = c;
+  }
+  ProjArgs p = pa;
+  const int64_t wg0 = (int64_t)((pa.N + 31) / 32) * pa.B, slots = (int64_t)per_cu * cus;
+  int best_g = 1;
+  double best = 1e300;
+  for (int g = 1; g <= pa.H; ++g) {
+    const int hpg = (pa.H + g - 1) / g;
+    if (g > 1 && (pa.H + hpg - 1) / hpg != g) continue;  // same hpg as a smaller g
+    const double cost = (double)((wg0 * g + slots - 1) / slots) * (hpg + 0.25);
+    if (cost < best - 1e-9) {
+      best = cost;
+      best_g = g;
+    }
+  }
+  p.hpg = (pa.H + best_g - 1) / best_g;
+  const int ng = (pa.H + p.hpg - 1) / p.hpg;
+  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
+                     dim3(64 * 3 * NBD), lds, stream, p);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 

@@ -112,6 +112,7 @@ struct ProjArgs {
   float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
   int B, N, H, D, nbk, Cpad, bfloat;
   int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
+  int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
   RowsPrepArgs rq, rk;  // q / k row outputs (rows_prep layout)
   ColsPrepArgs cv;      // V outputs (cols_prep layout)
 };
@@ -148,7 +149,7 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   return L;
 }
 
-// One workgroup per (32-token block, image), looping over the heads; 3 * NBD waves,
+// One workgroup per (32-token block, image, head group), looping over the group's heads; 3 * NBD waves,
 // wave (s, cb) = sub-matrix s (q, k, v) and its 32-column block cb of the head.
 #ifndef MXA_PROJ_WAVES
 #define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
@@ -226,7 +227,8 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
   const int8_t* xa = xt + ln * L.xst + kh;
   const int64_t hrow_b = (int64_t)b * a.H;
 
-  for (int h = 0; h < a.H; ++h) {
+  const int h_end = min(a.H, ((int)blockIdx.z + 1) * a.hpg);
+  for (int h = (int)blockIdx.z * a.hpg; h < h_end; ++h) {
     // ---- this wave's 32 x 32 output block of head h -------------------------------
     const int64_t blkc = (int64_t)(s * a.H + h) * NBD + cb;  // padded 32-column block
     const int64_t pc = 32 * blkc + ln;
@@ -254,14 +256,22 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
       for (int i = 0; i < 16; ++i) acc[i] = 0;
       v4i_ b0 = *reinterpret_cast<const v4i_*>(wp);
       v4i_ b1 = nbk > 1 ? *reinterpret_cast<const v4i_*>(wp + 1024) : b0;
+      // the column's block exponents ride two K-blocks ahead with the weight codes (a
+      // load per block issued right before its use left an L2 round trip on every step)
+      int16_t e0 = wep[0], e1 = nbk > 1 ? wep[1] : e0;
       for (int kb = 0; kb < nbk; ++kb) {
         const v4i_ bv = b0;
+        const int16_t ewr = e0;
         b0 = b1;
-        if (kb + 2 < nbk) b1 = *reinterpret_cast<const v4i_*>(wp + (kb + 2) * 1024);
+        e0 = e1;
+        if (kb + 2 < nbk) {
+          b1 = *reinterpret_cast<const v4i_*>(wp + (kb + 2) * 1024);
+          e1 = wep[kb + 2];
+        }
         const v4i_ av = *reinterpret_cast<const v4i_*>(xa + 32 * kb);
         const v16i zero = {};
         const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
-        int ew = exp_from16(wep[kb]);
+        int ew = exp_from16(ewr);
         cnan = cnan || ew == kExpNaN;
         ew = ew == kExpNaN ? wlo : ew;
         const int16_t* eb = xe + kb * 32 + m0;
@@ -300,25 +310,28 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
     else run(std::integral_constant<bool, false>{});
     __syncthreads();
 
-    // ---- q and k rows: rows_prep's per-block body on the tile (2 lanes per block) ----
+    // ---- q and k rows (waves 0 .. 2 NBD - 1) beside V's columns (the other NBD waves:
+    // 64 NBD >= D lanes, one column each).  Before, the wave that took the first q rows
+    // then took V as well while the rest waited at the barrier.
     const int64_t hrow0 = (hrow_b + h) * a.N + n0;  // row of (b, h, n0) in the q / k tables
     constexpr int kPer = 32 * NBD * 2;              // lanes per sub-matrix: a multiple of 64
-#pragma unroll 1
-    for (int t0 = 0; t0 < 2 * kPer; t0 += kThreads) {
-      const int t = t0 + (int)threadIdx.x;
-      const bool tv = t < 2 * kPer;
-      const int sk = __builtin_amdgcn_readfirstlane(tv ? t / kPer : 0);  // uniform per wave: q or k
-      const int rem = tv ? t - sk * kPer : 0;
+    static_assert(kThreads - 2 * kPer == 64 * NBD, "V lanes");
+    if ((int)threadIdx.x < 2 * kPer) {
+      // rows_prep's per-block body on the tile (2 lanes per 32-element block)
+      const int t = (int)threadIdx.x;
+      const int sk = __builtin_amdgcn_readfirstlane(t / kPer);  // uniform per wave: q or k
+      const int rem = t - sk * kPer;
       const int g = rem >> 1, sub = rem & 1;
       const int m = g / NBD, blk = g - m * NBD;
       const int c0 = 32 * blk + 16 * sub;
       float xv[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) xv[j] = (tv && c0 + j < D) ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
-      rows_prep_block<16>(sk ? a.rk : a.rq, hrow0 + m, blk, sub, c0, xv, tv && m < rows);
-    }
-    // ---- V: cols_prep's per-column body over the 32 tokens -------------------------
-    for (int c = threadIdx.x; c < D; c += kThreads) {
+      for (int j = 0; j < 16; ++j) xv[j] = c0 + j < D ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
+      const RowsPrepArgs& ra = sk ? a.rk : a.rq;
+      if (rows_prep_plain(ra)) rows_prep_block_plain<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+      else rows_prep_block<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+    } else if (const int c = (int)threadIdx.x - 2 * kPer; c < D) {
+      // V: cols_prep's per-column body over the 32 tokens
       float xv[32];
       uint32_t mx = 0;
 #pragma unroll
