@@ -154,6 +154,9 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #ifndef MXA_PROJ_WAVES
 #define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
 #endif
+#ifndef MXA_PROJ_PF
+#define MXA_PROJ_PF 2  // K-blocks of weight codes in flight per wave (measured: 4 and 8 slower, registers)
+#endif
 template <int NBD>
 __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -254,21 +257,33 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
       typename std::conditional<FAST, int, double>::type acc[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0;
-      v4i_ b0 = *reinterpret_cast<const v4i_*>(wp);
-      v4i_ b1 = nbk > 1 ? *reinterpret_cast<const v4i_*>(wp + 1024) : b0;
-      // the column's block exponents ride two K-blocks ahead with the weight codes (a
-      // load per block issued right before its use left an L2 round trip on every step)
-      int16_t e0 = wep[0], e1 = nbk > 1 ? wep[1] : e0;
+      // the weight codes and the column's block exponents ride kPf K-blocks ahead (a
+      // load per block issued right before its use left an L2 round trip on every
+      // step), the x operand one block ahead
+      constexpr int kPf = MXA_PROJ_PF;
+      v4i_ bq[kPf];
+      int16_t eq[kPf];
+#pragma unroll
+      for (int i = 0; i < kPf; ++i) {
+        const int kk = i < nbk ? i : 0;
+        bq[i] = *reinterpret_cast<const v4i_*>(wp + kk * 1024);
+        eq[i] = wep[kk];
+      }
+      v4i_ an = *reinterpret_cast<const v4i_*>(xa);
       for (int kb = 0; kb < nbk; ++kb) {
-        const v4i_ bv = b0;
-        const int16_t ewr = e0;
-        b0 = b1;
-        e0 = e1;
-        if (kb + 2 < nbk) {
-          b1 = *reinterpret_cast<const v4i_*>(wp + (kb + 2) * 1024);
-          e1 = wep[kb + 2];
+        const v4i_ bv = bq[0];
+        const int16_t ewr = eq[0];
+#pragma unroll
+        for (int i = 0; i + 1 < kPf; ++i) {
+          bq[i] = bq[i + 1];
+          eq[i] = eq[i + 1];
         }
-        const v4i_ av = *reinterpret_cast<const v4i_*>(xa + 32 * kb);
+        if (kb + kPf < nbk) {
+          bq[kPf - 1] = *reinterpret_cast<const v4i_*>(wp + (kb + kPf) * 1024);
+          eq[kPf - 1] = wep[kb + kPf];
+        }
+        const v4i_ av = an;
+        if (kb + 1 < nbk) an = *reinterpret_cast<const v4i_*>(xa + 32 * (kb + 1));
         const v16i zero = {};
         const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
         int ew = exp_from16(ewr);
