@@ -45,6 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MXINT8 attn fwd tokens/s/GPU (DeiT-base, DiT-XL/2); top-k idx bit-match"
+PROFILE_TAG = "r03"  # the round whose committed PMC profiles the bench line cites
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: dense I8 MFMA = 2x BF16 (~2.5 PF) per clock
 
@@ -147,6 +148,29 @@ def shard(c, rank, world, scaling):
 _CPU_INPUTS = None  # images of the CPU-baseline sample, made before the pool forks
 
 
+def usable_cores():
+    """Every core this process may run on: the affinity mask, capped by the cgroup CPU
+    quota when one is set (cpu.max; a GPU box's share of a large host shows all the
+    host's CPUs in nproc and the affinity mask but runs on its quota only)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is None:
+        for var in ("OMP_NUM_THREADS",):  # the box's advertised share when no quota file exists
+            v = os.environ.get(var, "")
+            if v.isdigit() and int(v) > 0 and int(v) < aff:
+                quota = int(v)
+    cores = min(aff, quota) if quota else aff
+    return cores, (f"nproc {os.cpu_count()}, affinity {aff}, cgroup/allotment quota {quota}: "
+                   f"{cores} worker processes, every usable core")
+
+
 def _oracle_image(i):
     from threadpoolctl import threadpool_limits
     from oracle import mx_oracle as O
@@ -167,7 +191,7 @@ def cpu_baseline(c, images):
     global _CPU_INPUTS
     import multiprocessing as mp
     import torch
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, why = usable_cores()
     _CPU_INPUTS = (c, make_inputs(c, list(range(images))))
     _oracle_image(0)  # warm: loads the oracle library before the fork
     with mp.get_context("fork").Pool(cores) as pool:
@@ -178,7 +202,7 @@ def cpu_baseline(c, images):
     return {"value": images * c["N"] / dt, "unit": "tokens/s", "cores": cores, "kind": "port",
             "sample": f"{images} images x {c['H']} heads of the {c['workload']} workload, same synthetic inputs; "
                       f"oracle/mx_oracle.py (numpy float32 + libstdc++ top-k), {cores} worker processes x 1 thread "
-                      f"(nproc {os.cpu_count()}, usable {len(os.sched_getaffinity(0))}, torch threads "
+                      f"({why}; torch threads "
                       f"{torch.get_num_threads()} unused by the oracle), {dt:.2f} s wall, {busy:.1f} s of CPU work"}
 
 
@@ -219,7 +243,75 @@ def timed_region(run, world, sync, device):
     return elapsed
 
 
-def run_config(c, images, steps, warmup, device, world, traffic_json=None):
+SIMDS = 1024            # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs
+CLK_HZ = 2.4e9          # max engine clock (the chip runs lower under load: the VALU fraction is a floor)
+VALU_ISSUE_CYC = 2      # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+
+
+def _unique_kernel(d, stage):
+    """The one kernel instantiation of `stage` in a per-kernel profile dict, or None
+    (several instantiations never average together: tools/hbm_traffic.py)."""
+    names = [n for n in d if stage_of_kernel(n) == stage]
+    return names[0] if len(names) == 1 else None
+
+
+def stage_of_kernel(name):
+    if "select_kernel" in name:
+        return "select"
+    if "finish_kernel" in name or "dense_rows_kernel" in name:
+        return "finish"
+    if "attn_prep_kernel" in name:
+        return "prep"
+    if "qkv_proj_kernel" in name:
+        return "proj"
+    return None
+
+
+def profile_of(prof, stage, ms, ach_gbs):
+    """(traffic bytes per launch or None, limiter block) of the dominant kernel from the
+    committed profiles of this config: PMC HBM traffic (tools/hbm_traffic.py output) and
+    instruction counters (tools/pmc_summary.py --json output).  bound = the resource with
+    the largest measured busy fraction among HBM (PMC traffic / time / peak), VALU issue
+    (VALU instructions x 2 cycles / (SIMDs x clock x time)) and MFMA (busy cycles)."""
+    prof = prof or {}
+    traffic = None
+    lim = {"bound": "hbm", "source": None, "fracs": {"hbm_algorithmic": ach_gbs / HBM_PEAK_GBS}}
+    tj = prof.get("traffic")
+    if tj and os.path.exists(tj):
+        with open(tj) as fh:
+            t = json.load(fh)
+        traffic = t.get("stages", {}).get(stage)
+        if traffic is not None:
+            lim["fracs"]["hbm_measured"] = traffic / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
+        lim["source"] = os.path.relpath(tj, ROOT)
+    pj = prof.get("pmc")
+    if pj and os.path.exists(pj):
+        with open(pj) as fh:
+            pm = json.load(fh)
+        name = _unique_kernel(pm, stage)
+        if name:
+            k = pm[name]
+            sec = ms * 1e-3
+            if "SQ_INSTS_VALU" in k:
+                lim["fracs"]["valu_issue"] = k["SQ_INSTS_VALU"] * VALU_ISSUE_CYC / (SIMDS * CLK_HZ * sec)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in k:  # counted in cycles, summed over SIMDs
+                lim["fracs"]["mfma_busy"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * CLK_HZ * sec)
+            if "SQ_WAIT_ANY" in k and "SQ_WAVE_CYCLES" in k and k["SQ_WAVE_CYCLES"]:
+                lim["wait_any_share"] = k["SQ_WAIT_ANY"] / k["SQ_WAVE_CYCLES"]
+            if "SQ_LDS_BANK_CONFLICT" in k and k.get("SQ_INSTS_LDS"):
+                lim["lds_conflict_cycles_per_lds_instr"] = k["SQ_LDS_BANK_CONFLICT"] / k["SQ_INSTS_LDS"]
+            lim["kernel"] = name
+            lim["pmc_source"] = os.path.relpath(pj, ROOT)
+    f = lim["fracs"]
+    cand = {"hbm": max(f.get("hbm_measured", 0.0), f["hbm_algorithmic"]), "valu": f.get("valu_issue", 0.0),
+            "mfma": f.get("mfma_busy", 0.0)}
+    lim["bound"] = max(cand, key=cand.get)
+    if lim["bound"] != "mfma" and max(cand.values()) < 0.5 and lim.get("wait_any_share", 0.0) > 0.3:
+        lim["bound"] = "latency"  # no unit near its peak and the waves mostly parked
+    return traffic, lim
+
+
+def run_config(c, images, steps, warmup, device, world, prof=None):
     """Time `steps` calls of the op on this rank's images; returns the elapsed time
     (max over ranks), the stage times, the roofline block and the outputs."""
     import torch
@@ -263,18 +355,14 @@ def run_config(c, images, steps, warmup, device, world, traffic_json=None):
     by = stage_bytes(cb, path)
     dom = max(stages, key=stages.get)
     ach = by[dom] / (stages[dom] * 1e-3) / 1e9
-    traffic = None
-    if traffic_json and os.path.exists(traffic_json):
-        traffic = json.load(open(traffic_json)).get(dom)
+    traffic, lim = profile_of(prof, dom, stages[dom], ach)
     qa_ms = stages["prep"] + stages["select"]
     qa_gbs = bytes_qa(cb) / (qa_ms * 1e-3) / 1e9
     mf_tops = ops_gemm(cb) / (stages["finish"] * 1e-3) / 1e12
     roof = {
-        "bound": "hbm", "kernel": dom, "path": path,
-        "limiter": ("instruction issue (VALU + LDS) of the exact-order top-k: the selection kernel moves "
-                    "~2% of its duration's HBM bytes (PMC: profiles/r02_*)") if dom == "select" else
-                   ("VALU: v_dot4 gather of the kept keys' true scores (fp64 block epilogue), softmax, MX(P)"
-                    if dom == "finish" else None),
+        # bound: the resource the PMC profile shows limiting the dominant kernel; the
+        # achieved / peak / frac below are its HBM roofline (algorithmic bytes / time)
+        "bound": lim["bound"], "frac_of": "hbm", "kernel": dom, "path": path, "limiter": lim,
         "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
         "algorithmic_bytes_per_launch": by[dom], "mean_ms": stages[dom],
         "qa_pass": {"what": "SURVEY §8d Bytes_qa over the prep (Q, K, V) + selection kernels",
@@ -338,6 +426,43 @@ def run_qkv(c, images, steps, warmup, device, world):
     return elapsed, stages, extra
 
 
+def run_secondary(args, c, rank, world, images, lines, run, device, res=None):
+    """The secondary lines: `qkv` (the config's fused qkv-Linear line) and `dit` (the
+    DiT-XL/2 line of deit_base).  With res None (no main line: profiling passes) the
+    secondaries go out as their own JSON line."""
+    import torch.distributed as dist
+    alone = res is None
+    if alone:
+        res = {"metric": METRIC, "lines": sorted(lines)}
+    if args.config in ("deit_base", "dit_xl2") and "qkv" in lines and run is run_config:
+        # the qkv mx.Linear fused in front (SURVEY §8f row 1): x (B, N, C) -> out + idx
+        qsteps = max(args.steps // 2, 1)
+        qel, qst, qex = run_qkv(c, images, qsteps, 2, device, world)
+        qtok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * qsteps
+        res.setdefault("secondary", []).append(
+            {"config": args.config + "+qkv_linear", "workload": "mx.Linear qkv projection (C=%d -> 3C) fused into the "
+             "attention core's MX operands, then the same attention" % (c["H"] * c["D"]),
+             "value": qtok / qel, "unit": "tokens/s", "ms_per_step": qel / qsteps * 1e3, "stages_ms": qst, **qex})
+
+    if args.config == "deit_base" and "dit" in lines:
+        d = CONFIGS["dit_xl2"]
+        dimg = shard(d, rank, world, args.scaling)
+        dprof = {"traffic": os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_traffic_dit_xl2.json"),
+                 "pmc": os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_dit_xl2.json")}
+        delapsed, dst, droof, _, _, _ = run(d, dimg, max(args.steps // 2, 1), 2, device, world, dprof)
+        dtok = (world * d["B"] if args.scaling == "weak" else d["B"]) * d["N"] * max(args.steps // 2, 1)
+        res.setdefault("secondary", []).append({"config": "dit_xl2", "workload": d["workload"], "value": dtok / delapsed,
+                             "unit": "tokens/s", "ms_per_step": delapsed / max(args.steps // 2, 1) * 1e3,
+                             "batch_per_gpu": len(dimg), "stages_ms": dst, "roofline": droof})
+    if alone:
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.barrier()
+        return res if rank == 0 else 0
+    return res
+
+
 def launch_ranks(args):
     """--gpus N without WORLD_SIZE: start the N ranks (one process per GPU) through
     torch.distributed.run from this process, which has not touched the GPU, and exit
@@ -364,7 +489,15 @@ def main(argv=None, run=run_config):
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the DiT-XL/2 line")
     ap.add_argument("--parity-images", type=int, default=2, help="images per rank checked against the oracle")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per dominant-kernel launch")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC HBM traffic per kernel (tools/hbm_traffic.py; default: the committed "
+                         "profiles/<PROFILE_TAG>_traffic_<config>.json)")
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC instruction counters per kernel (tools/pmc_summary.py --json; default: the "
+                         "committed profiles/<PROFILE_TAG>_pmc_<config>.json)")
+    ap.add_argument("--lines", default="main,qkv,dit",
+                    help="which lines to run: main (the config), qkv (its fused qkv-Linear line), dit "
+                         "(the DiT-XL/2 secondary of deit_base)")
     args = ap.parse_args(argv)
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -393,7 +526,14 @@ def main(argv=None, run=run_config):
         dist.init_process_group(backend, **({"device_id": device} if backend == "nccl" else {}))
 
     images = shard(c, rank, world, args.scaling)
-    elapsed, stages, roof, e2e, out, idx = run(c, images, args.steps, args.warmup, device, world, args.traffic_json)
+    lines = set(args.lines.split(","))
+    if args.no_secondary:
+        lines &= {"main"}
+    prof = {"traffic": args.traffic_json or os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_traffic_{args.config}.json"),
+            "pmc": args.pmc_json or os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_{args.config}.json")}
+    if "main" not in lines:  # profiling the secondary lines alone
+        return run_secondary(args, c, rank, world, images, lines, run, device)
+    elapsed, stages, roof, e2e, out, idx = run(c, images, args.steps, args.warmup, device, world, prof)
     tokens = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * args.steps
     res = {
         "metric": METRIC,
@@ -438,25 +578,7 @@ def main(argv=None, run=run_config):
                                          torch.cat(gm).cpu().tolist())
             res["parity"]["ranks_checked"] = world
 
-    if args.config in ("deit_base", "dit_xl2") and not args.no_secondary and run is run_config:
-        # the qkv mx.Linear fused in front: x (B, N, C) -> out + idx
-        qsteps = max(args.steps // 2, 1)
-        qel, qst, qex = run_qkv(c, images, qsteps, 2, device, world)
-        qtok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * qsteps
-        res.setdefault("secondary", []).append(
-            {"config": args.config + "+qkv_linear", "workload": "mx.Linear qkv projection (C=%d -> 3C) fused into the "
-             "attention core's MX operands, then the same attention" % (c["H"] * c["D"]),
-             "value": qtok / qel, "unit": "tokens/s", "ms_per_step": qel / qsteps * 1e3, "stages_ms": qst, **qex})
-
-    if args.config == "deit_base" and not args.no_secondary:
-        d = CONFIGS["dit_xl2"]
-        dimg = shard(d, rank, world, args.scaling)
-        delapsed, dst, droof, _, _, _ = run(d, dimg, max(args.steps // 2, 1), 2, device, world, None)
-        dtok = (world * d["B"] if args.scaling == "weak" else d["B"]) * d["N"] * max(args.steps // 2, 1)
-        res.setdefault("secondary", []).append({"config": "dit_xl2", "workload": d["workload"], "value": dtok / delapsed,
-                             "unit": "tokens/s", "ms_per_step": delapsed / max(args.steps // 2, 1) * 1e3,
-                             "batch_per_gpu": len(dimg), "stages_ms": dst,
-                             "roofline_frac": droof["frac"], "qa_pass_frac": droof["qa_pass"]["frac"]})
+    run_secondary(args, c, rank, world, images, lines, run, device, res)
 
     if rank == 0:
         print(json.dumps(res), flush=True)

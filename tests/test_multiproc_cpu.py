@@ -30,7 +30,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _stub_run(c, images, steps, warmup, device, world, traffic_json):
+def _stub_run(c, images, steps, warmup, device, world, prof):
     """CPU stand-in for run_config: the op's outputs from the oracle, a timed region of
     rank-dependent length."""
     import bench
@@ -119,13 +119,59 @@ def test_bench_byte_and_op_accounting():
 
 
 def test_hbm_traffic_kernel_names_map_to_bench_stages():
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("hbm_traffic", os.path.join(ROOT, "tools", "hbm_traffic.py"))
-    ht = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(ht)
+    ht = _load_hbm_traffic()
     assert ht.stage_of("void mxa::select_kernel<256, 3>(mxa::Rows2Args)") == "select"
     assert ht.stage_of("void mxa::finish_kernel<2, 2>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("void mxa::dense_rows_kernel<4>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("mxa::attn_prep_kernel(mxa::RowsPrepArgs, mxa::RowsPrepArgs, mxa::ColsPrepArgs, unsigned int, "
                        "unsigned int)") == "prep"
     assert ht.stage_of("void mxa::qkv_proj_kernel<2>(mxa::ProjArgs)") == "proj"
+
+
+def _load_hbm_traffic():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("hbm_traffic", os.path.join(ROOT, "tools", "hbm_traffic.py"))
+    ht = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ht)
+    return ht
+
+
+def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
+    """Round 2's DeiT select traffic was the average of DeiT's select_kernel<256,3,2> and
+    DiT's select_kernel<256,3,4> dispatches: per-instantiation keys keep them apart, and a
+    stage with two instantiations in one run gets no traffic number at all."""
+    ht = _load_hbm_traffic()
+    deit, dit = "void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)", "void mxa::select_kernel<256, 3, 4>(mxa::Rows2Args)"
+    fin = "void mxa::finish_kernel<2, 12, true>(mxa::Rows2Args)"
+    rows = []
+    for name, kib_f, kib_w, n in ((deit, 10.0, 143250.0, 7), (dit, 20.0, 473145.0, 3), (fin, 100.0, 200.0, 7)):
+        for _ in range(n):
+            rows.append({"Kernel_Name": name, "Counter_Name": "FETCH_SIZE", "Counter_Value": str(kib_f)})
+            rows.append({"Kernel_Name": name, "Counter_Name": "WRITE_SIZE", "Counter_Value": str(kib_w)})
+    out = ht.combine(ht.per_kernel(rows, "FETCH_SIZE"), ht.per_kernel(rows, "WRITE_SIZE"))
+    assert out["kernels"][deit]["write_bytes"] == 143250.0 * 1024 and out["kernels"][deit]["dispatches"] == [7, 7]
+    assert out["kernels"][dit]["write_bytes"] == 473145.0 * 1024
+    assert out["kernels"][deit]["traffic_bytes"] == (2 * 10.0 + 143250.0) * 1024
+    assert "select" not in out["stages"] and sorted(out["ambiguous"]["select"]) == sorted([deit, dit])
+    assert out["stages"]["finish"] == (2 * 100.0 + 200.0) * 1024
+    # a run with one instantiation per stage maps every stage
+    one = ht.combine(ht.per_kernel(rows[:14], "FETCH_SIZE"), ht.per_kernel(rows[:14], "WRITE_SIZE"))
+    assert one["stages"] == {"select": (2 * 10.0 + 143250.0) * 1024} and not one["ambiguous"]
+
+
+def test_bench_limiter_from_profiles(tmp_path):
+    import bench
+    sel = "void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)"
+    tj, pj = tmp_path / "t.json", tmp_path / "p.json"
+    tj.write_text(json.dumps({"stages": {"select": 160e6}}))
+    # 0.5 ms: HBM 160 MB -> 0.04 of peak; VALU 436 M instr x 2 cycles over 1024 SIMDs at 2.4 GHz -> 0.71
+    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 436e6, "SQ_WAVE_CYCLES": 10.0, "SQ_WAIT_ANY": 4.0,
+                                    "SQ_LDS_BANK_CONFLICT": 5.0, "SQ_INSTS_LDS": 10.0}}))
+    traffic, lim = bench.profile_of({"traffic": str(tj), "pmc": str(pj)}, "select", 0.5, 320.0)
+    assert traffic == 160e6 and lim["bound"] == "valu" and lim["kernel"] == sel
+    assert abs(lim["fracs"]["valu_issue"] - 436e6 * 2 / (1024 * 2.4e9 * 0.5e-3)) < 1e-9
+    assert lim["lds_conflict_cycles_per_lds_instr"] == 0.5
+    # two instantiations of the stage in the PMC file: no kernel is picked
+    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("2>", "4>"): {"SQ_INSTS_VALU": 1.0}}))
+    _, lim = bench.profile_of({"pmc": str(pj)}, "select", 0.5, 320.0)
+    assert "kernel" not in lim and lim["bound"] == "hbm"

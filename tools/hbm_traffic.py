@@ -1,10 +1,20 @@
 """HBM bytes per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
 corrected as MI355X_MICROARCH.md (HBM section) prescribes for gfx950:
 FETCH_SIZE counts half the bytes of wide coalesced reads -> x2; WRITE_SIZE as is.
-Both counters are in KiB.  Output: {stage: bytes per launch} for bench.py
---traffic-json (stages as in bench.STAGES).
+Both counters are in KiB.
+
+Counters are kept per kernel INSTANTIATION (the full Kernel_Name, template arguments
+included) and averaged only over that instantiation's dispatches: two instantiations
+of one stage (e.g. DeiT's select_kernel<256,3,2> and DiT's select_kernel<256,3,4>)
+never average together.  A bench stage gets a traffic number only when exactly one
+instantiation maps to it in the profiled run; otherwise the stage is listed under
+"ambiguous" and bench.py reports traffic null for it.
 
   python tools/hbm_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
+
+Output: {"kernels": {name: {"fetch_bytes_x1", "write_bytes", "traffic_bytes",
+"dispatches", "fetch_spread", "write_spread"}}, "stages": {stage: bytes per launch},
+"ambiguous": {stage: [names]}, "note": ...}
 """
 import collections
 import csv
@@ -19,35 +29,70 @@ def stage_of(kernel):
         return "select"
     if "finish_kernel" in kernel or "dense_rows_kernel" in kernel:
         return "finish"
-    if "attn_prep_kernel" in kernel or "rows_prep_kernel" in kernel or "cols_prep_kernel" in kernel:
+    if "attn_prep_kernel" in kernel:
         return "prep"
     if "qkv_proj_kernel" in kernel:
         return "proj"
     return None
 
 
-def per_stage(d, counter):
+def per_kernel(rows, counter):
+    """{full kernel name: [bytes of each dispatch]} for one counter (KiB -> bytes)."""
     vals = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            st = stage_of(r["Kernel_Name"])
-            if st:
-                vals[st].append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+    for r in rows:
+        if r["Counter_Name"] == counter:
+            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    return vals
+
+
+def read_rows(d):
+    rows = []
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
+        with open(f) as fh:
+            rows.extend(csv.DictReader(fh))
+    return rows
+
+
+def spread(v):
+    m = sum(v) / len(v)
+    return (max(v) - min(v)) / m if m else 0.0
+
+
+def combine(fetch, write):
+    """Per-instantiation traffic and the per-stage mapping (see the module docstring)."""
+    kernels = {}
+    for name in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(name, []), write.get(name, [])
+        fb = sum(f) / len(f) if f else 0.0
+        wb = sum(w) / len(w) if w else 0.0
+        kernels[name] = {"fetch_bytes_x1": fb, "write_bytes": wb, "traffic_bytes": 2.0 * fb + wb,
+                         "dispatches": [len(f), len(w)], "fetch_spread": spread(f) if f else None,
+                         "write_spread": spread(w) if w else None}
+    by_stage = collections.defaultdict(list)
+    for name in kernels:
+        st = stage_of(name)
+        if st:
+            by_stage[st].append(name)
+    stages, ambiguous = {}, {}
+    for st, names in by_stage.items():
+        if len(names) == 1:
+            stages[st] = kernels[names[0]]["traffic_bytes"]
+        else:
+            ambiguous[st] = names
+    return {"kernels": kernels, "stages": stages, "ambiguous": ambiguous,
+            "note": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes, gfx950 correction), "
+                    "per launch, averaged over the dispatches of ONE kernel instantiation"}
 
 
 def main():
-    fetch = per_stage(sys.argv[1], "FETCH_SIZE")
-    write = per_stage(sys.argv[2], "WRITE_SIZE")
-    out = {}
-    for st in set(fetch) | set(write):
-        out[st] = 2.0 * fetch.get(st, 0.0) + write.get(st, 0.0)
-    out["_raw"] = {"fetch_bytes_x1": fetch, "write_bytes": write,
-                   "note": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 correction"}
-    json.dump(out, open(sys.argv[3], "w"), indent=1)
-    print(json.dumps(out))
+    fetch = per_kernel(read_rows(sys.argv[1]), "FETCH_SIZE")
+    write = per_kernel(read_rows(sys.argv[2]), "WRITE_SIZE")
+    out = combine(fetch, write)
+    with open(sys.argv[3], "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out["stages"]))
+    if out["ambiguous"]:
+        print("ambiguous stages (several instantiations): " + json.dumps(out["ambiguous"]), file=sys.stderr)
 
 
 if __name__ == "__main__":
