@@ -13,8 +13,15 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmxa.so")
-SOURCES = ["mxa_quant.hip", "mxa_attn.hip"]
-HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_finish.hpp", "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "../../include/mxa.h"]
+# (source, object suffix, defines): mxa_sel.hip is compiled three times, one part of the
+# selection kernel's instantiations each (MXA_SEL_PART), so that the parts build in parallel
+UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", "", ("MXA_SEL_PART=0",)),
+         ("mxa_sel.hip", "_p1", ("MXA_SEL_PART=1",)), ("mxa_sel.hip", "_p2", ("MXA_SEL_PART=2",)),
+         ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ())]
+SOURCES = sorted({u[0] for u in UNITS})
+HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
+           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
+           "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -33,16 +40,19 @@ def build(force=False, verbose=True, defines=(), tag=""):
     lib = LIB.replace("libmxa.so", f"libmxa_{tag}.so") if tag else LIB
     if not force and not _stale(lib):
         return lib
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", f"{'_' + tag if tag else ''}.o"))
+    objs, procs = [], []
+    for src, suffix, unit_defs in UNITS:  # one hipcc per translation unit, in parallel
+        obj = os.path.join(CSRC, src.replace(".hip", f"{suffix}{'_' + tag if tag else ''}.o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                "-Wall", "-Wno-unused-function", "-I", os.path.join(HERE, "..", "include"),
-               "-c", os.path.join(CSRC, src), "-o", obj] + [f"-D{d}" for d in defines]
+               "-c", os.path.join(CSRC, src), "-o", obj] + [f"-D{d}" for d in tuple(unit_defs) + tuple(defines)]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+        procs.append(subprocess.Popen(cmd))
         objs.append(obj)
+    bad = [p.args for p in procs if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, bad[0])
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -12,40 +12,37 @@
 // This is the mx_quant branch of the patched attention forward:
 //   workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
 //   workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859.
-#include "mxa_kernels.hpp"
-#include "mxa_order.hpp"
+#include "mxa_launch.hpp"
 
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
 
+
+
 namespace mxa {
 
-constexpr int kMaxNB = 4;  // head dim <= 128
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef int v4i_ __attribute__((ext_vector_type(4)));
 
-enum RowsMode : int {
-  kModeTrue = 0,   // row values are the true scores (approx off, or dense)
-  kModeOpExp = 1,  // approximator codes, block scale 2^(sa + sb)
-  kModeOpMul = 2,  // approximator codes, block scale sa * sb / 4096 (EXION)
-  kModeExSign = 3,  // ex_pred: sign words + block exponents
-  kModeTrueEx = 4,  // true_ex: power-of-two codes + zero indicators + block exponents
-  kModeElsa = 5     // ELSA: hash words, key norms, cosine table
-};
-
-// scalar (uniform-address) loads of a wave's query row
-typedef __attribute__((address_space(4))) const uint32_t* cu32;
-__device__ __forceinline__ int s_exp16(const int16_t* base, int64_t i) {
-  const uint32_t d = ((cu32)(base + (i & ~(int64_t)1)))[0];
-  return exp_from16((int16_t)(i & 1 ? d >> 16 : d & 0xFFFFu));
+// Self-test of the v_mfma_i32_32x32x32_i8 lane maps of the finishing kernel's P.V: A (32x32 row-major
+// M x K), B (32x32 row-major K x N) -> C (32x32 row-major) through the same maps.
+__global__ void selftest_mfma32_kernel(const int8_t* A, const int8_t* B, int32_t* C) {
+  const int lane = threadIdx.x, ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
+  v4i_ a4, b4;
+  for (int w = 0; w < 4; ++w) {
+    uint32_t x = 0, y = 0;
+    for (int j = 0; j < 4; ++j) {
+      x |= (uint32_t)(uint8_t)A[ln * 32 + kh + 4 * w + j] << (8 * j);
+      y |= (uint32_t)(uint8_t)B[(kh + 4 * w + j) * 32 + ln] << (8 * j);
+    }
+    a4[w] = (int)x;
+    b4[w] = (int)y;
+  }
+  const v16i zero = {};
+  const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a4, b4, zero, 0, 0, 0);
+  for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + m0 + (i & 3)) * 32 + ln] = c[i];
 }
-
-}  // namespace mxa
-
-#include "mxa_rows2.hpp"
-#include "mxa_finish.hpp"
-#include "mxa_proj.hpp"
-
-namespace mxa {
 
 // ---- mx.matmul: C[b] = MX(A[b], along K) @ MX(B[b], along K) ---------------
 struct MatmulArgs {
@@ -165,7 +162,6 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
   return L;
 }
 
-bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
 
 }  // namespace
 
@@ -186,222 +182,6 @@ extern "C" int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p) {
   if (!p || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return -1;
   // sized for the approximator whenever it may run (top-k, or the scores alone)
   return attn_layout(p, score_mode(p, p->top_k || p->pred_out)).total;
-}
-
-// ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
-static size_t rows2_total(const Rows2Args& ra, int W) {
-  return rows2_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.tpad, W).total;
-}
-// waves per workgroup: the size (8 or 16) that keeps the most waves resident per CU
-// (LDS-limited workgroups x waves, capped by the kernel's 7-waves-per-SIMD register use)
-static int rows2_waves(const Rows2Args& ra) {
-  auto resident = [&](int w) {
-    const size_t t = rows2_total(ra, w);
-    return t > 160 * 1024 ? 0 : std::min((int)(160 * 1024 / t) * w, 28);
-  };
-  const int r8 = resident(8), r16 = resident(16);
-  if (r8 > 0 || r16 > 0) return r16 > r8 ? 16 : 8;
-  return rows2_total(ra, 4) <= 160 * 1024 ? 4 : 0;
-}
-
-template <int S>
-static int launch_dense_s(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
-  Rows2Args ra = ra0;
-  ra.waves = rows2_waves(ra);
-  if (ra.waves <= 0) return MXA_ERR_UNSUPPORTED;
-  if (plan) return MXA_OK;
-  const size_t lds = rows2_total(ra, ra.waves);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&dense_rows_kernel<S>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  // few heads: split each head's rows over grid.y so that the launch still has ~4
-  // workgroups per CU
-  const int chunks = std::max(1, std::min((ra.N + ra.waves - 1) / ra.waves, 1024 / std::max(BH, 1)));
-  ra.rows_per_wg = (ra.N + chunks - 1) / chunks;
-  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL(dense_rows_kernel<S>, dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-
-// ---- selection kernel (mxa_select.hpp): four query rows per wave -------------------
-template <int NP, int MODE, int W>
-static size_t select_lds(const Rows2Args& ra) {
-  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP);
-}
-template <int NP, int MODE, int W>
-static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
-  Rows2Args ra = ra0;
-  const size_t lds = select_lds<NP, MODE, W>(ra);
-  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  if (plan) return MXA_OK;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
-  int rows = kSelRows;
-  while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
-  ra.rows_per_wg = rows;
-  const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_kernel<NP, MODE, W>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-template <int NP, int MODE>
-static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
-  return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
-}
-template <int MODE>
-static int launch_select_m(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (ra.T <= 128) return launch_select_np<128, MODE>(ra, BH, stream, plan);
-  if (ra.T <= 256) return launch_select_np<256, MODE>(ra, BH, stream, plan);
-  return launch_select_np<512, MODE>(ra, BH, stream, plan);
-}
-static int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
-  switch (mode) {
-    case kModeOpExp: return launch_select_m<kModeOpExp>(ra, BH, stream, plan);
-    case kModeOpMul: return launch_select_m<kModeOpMul>(ra, BH, stream, plan);
-    case kModeExSign: return launch_select_m<kModeExSign>(ra, BH, stream, plan);
-    case kModeTrueEx: return launch_select_m<kModeTrueEx>(ra, BH, stream, plan);
-    case kModeElsa: return launch_select_m<kModeElsa>(ra, BH, stream, plan);
-    default: return launch_select_m<kModeTrue>(ra, BH, stream, plan);
-  }
-}
-
-// ---- finishing kernel (mxa_finish.hpp): 32-row MFMA tiles, one per wave ------------
-// two lanes per query row (one pass per tile) when every row's kept keys fit 2 x 16 slots
-static bool finish_pair(const Rows2Args& ra) { return ra.k_top <= 32; }
-static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg) {
-  const int tiles = (ra.N + kFinTile - 1) / kFinTile;
-  const bool pair = finish_pair(ra);
-  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, pair).total; };
-  if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  // a head's tiles round-robin over the waves of one workgroup (the K / V tables
-  // staged once per head); few heads (PixArt cross-attention): the tiles split over
-  // grid.y so that the grid still has ~2 workgroups per CU
-  int chunks = 1;
-  while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
-  // waves per workgroup: the fewest sequential tile rounds per CU -- workgroups per
-  // CU over the LDS-limited concurrency, times each workgroup's rounds over its
-  // tiles; ties to the smaller workgroup (measured: DeiT-base 4 waves, 2 workgroups
-  // per CU, 0.29 ms vs 0.36 ms with 5; DiT 8 waves, 0.36 ms vs 0.61 ms with 4)
-  const int tpc = (tiles + chunks - 1) / chunks;
-  const int64_t wgs_per_cu = ((int64_t)BH * chunks + 255) / 256;
-  int w = 1;
-  int64_t best = -1;
-  for (int c = 1; c <= std::min(8, tpc); ++c) {
-    const size_t t = lds(c);
-    if (t > 160 * 1024) break;
-    const int64_t conc = std::min<int64_t>(160 * 1024 / t, 12 / c > 0 ? 12 / c : 1);
-    const int64_t score = (wgs_per_cu + conc - 1) / conc * ((tpc + c - 1) / c);
-    if (best < 0 || score < best) best = score, w = c;
-  }
-  *waves = w;
-  *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
-  return MXA_OK;
-}
-template <int NB, int KS, bool PAIR>
-static int launch_finish_ks(const Rows2Args& ra0, int BH, hipStream_t stream) {
-  Rows2Args ra = ra0;
-  int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
-  if (rc) return rc;
-  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR).total;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-template <int NB>
-static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
-  if (finish_pair(ra)) {  // slots per lane: ceil(k / 2)
-    const int kp = (ra.k_top + 1) / 2;
-    if (kp <= 2) return launch_finish_ks<NB, 2, true>(ra, BH, stream);
-    if (kp <= 4) return launch_finish_ks<NB, 4, true>(ra, BH, stream);
-    if (kp <= 8) return launch_finish_ks<NB, 8, true>(ra, BH, stream);
-    if (kp <= 12) return launch_finish_ks<NB, 12, true>(ra, BH, stream);
-    return launch_finish_ks<NB, 16, true>(ra, BH, stream);
-  }
-  const int ks = (ra.k_top + 15) / 16;
-  if (ks <= 1) return launch_finish_ks<NB, 1, false>(ra, BH, stream);
-  if (ks <= 2) return launch_finish_ks<NB, 2, false>(ra, BH, stream);
-  if (ks <= 4) return launch_finish_ks<NB, 4, false>(ra, BH, stream);
-  if (ks <= 8) return launch_finish_ks<NB, 8, false>(ra, BH, stream);
-  if (ks <= 16) return launch_finish_ks<NB, 16, false>(ra, BH, stream);
-  return launch_finish_ks<NB, 32, false>(ra, BH, stream);
-}
-static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (plan) {
-    int w, r;
-    return finish_plan(ra, BH, &w, &r);
-  }
-  switch (ra.nbd) {
-    case 1: return launch_finish_nb<1>(ra, BH, stream);
-    case 2: return launch_finish_nb<2>(ra, BH, stream);
-    case 3: return launch_finish_nb<3>(ra, BH, stream);
-    default: return launch_finish_nb<4>(ra, BH, stream);
-  }
-}
-
-// the row kernel of the path: the finishing kernel (top-k) or the dense kernel
-static int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan) {
-  if (topk) {
-    // the selection kernel already wrote the true scores when it ranked them
-    Rows2Args rf = ra;
-    if (true_mode) rf.true_out = nullptr;
-    return launch_finish(rf, BH, stream, plan);
-  }
-  switch (S) {
-    case 1: return launch_dense_s<1>(ra, BH, stream, plan);
-    case 2: return launch_dense_s<2>(ra, BH, stream, plan);
-    case 4: return launch_dense_s<4>(ra, BH, stream, plan);
-    default: return launch_dense_s<8>(ra, BH, stream, plan);
-  }
-}
-
-// ---- fused qkv projection (mxa_proj.hpp) ------------------------------------------
-template <int NBD>
-static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
-  const size_t lds = proj_lds(pa.Cpad, pa.nbk, pa.D).total;
-  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  // head groups: a workgroup loops over hpg heads after staging its x tile once; the
-  // group count minimises (rounds of resident workgroups) x (heads + ~1/4 head of x
-  // staging) -- with all heads per workgroup DeiT-base's 1,792 workgroups ran 3.5
-  // rounds of 512 resident ones, the last half empty
-  static int per_cu = -1, cus = -1;
-  static size_t lds_q = 0;  // the LDS size the occupancy was queried for
-  if (per_cu < 0 || lds_q != lds) {
-    lds_q = lds;
-    int dev = 0, n = 0, c = 0;
-    (void)hipGetDevice(&dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
-                                                     64 * 3 * NBD, lds) != hipSuccess || n < 1)
-      n = 1;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
-    per_cu = n;
-    cus = c;
-  }
-  ProjArgs p = pa;
-  const int64_t wg0 = (int64_t)((pa.N + 31) / 32) * pa.B, slots = (int64_t)per_cu * cus;
-  int best_g = 1;
-  double best = 1e300;
-  for (int g = 1; g <= pa.H; ++g) {
-    const int hpg = (pa.H + g - 1) / g;
-    if (g > 1 && (pa.H + hpg - 1) / hpg != g) continue;  // same hpg as a smaller g
-    const double cost = (double)((wg0 * g + slots - 1) / slots) * (hpg + 0.25);
-    if (cost < best - 1e-9) {
-      best = cost;
-      best_g = g;
-    }
-  }
-  p.hpg = (pa.H + best_g - 1) / best_g;
-  const int ng = (pa.H + p.hpg - 1) / p.hpg;
-  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
-                     dim3(64 * 3 * NBD), lds, stream, p);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
 // x -> MX codes along C (rows_prep), then the projection kernel writing the q / k
@@ -433,12 +213,7 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   pa.smax = -1;
   while ((int64_t)nbk * 516128 * ((int64_t)1 << (pa.smax + 1)) < ((int64_t)1 << 31)) ++pa.smax;
   pa.rq = rq; pa.rk = rk; pa.cv = cv;
-  switch ((pp.D + 31) / 32) {
-    case 1: return launch_proj_nbd<1>(pa, stream);
-    case 2: return launch_proj_nbd<2>(pa, stream);
-    case 3: return launch_proj_nbd<3>(pa, stream);
-    default: return launch_proj_nbd<4>(pa, stream);
-  }
+  return launch_proj(pa, stream);
 }
 
 // plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing;
@@ -597,38 +372,6 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   return MXA_OK;
 }
 
-extern "C" int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features, int32_t group_width) {
-  if (out_features <= 0 || in_features <= 0 || group_width <= 0 || out_features % group_width) return -1;
-  return linear_layout(out_features, in_features, group_width).total;
-}
-
-extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_features, int32_t group_width,
-                                      int32_t flush_subnormals, int32_t bfloat, void* wq, hipStream_t stream) {
-  if (!w || !wq || out_features <= 0 || in_features <= 0 || group_width <= 0 || out_features % group_width)
-    return MXA_ERR_ARG;
-  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
-  if (!aligned16(wq)) return MXA_ERR_ARG;
-  const LinearLayout W = linear_layout(out_features, in_features, group_width);
-  unsigned char* wb = static_cast<unsigned char*>(wq);
-  RowsPrepArgs rw{};
-  rw.x = w; rw.s0 = 0; rw.s1 = 0; rw.s2 = in_features;
-  rw.H = 1; rw.R = out_features; rw.rows = out_features; rw.D = in_features; rw.nb = W.nbk; rw.dpad = W.Cpad;
-  rw.vec4 = aligned16(w) && in_features % 4 == 0;
-  rw.op_kind = MXA_OP_MXINT8; rw.flush = flush_subnormals; rw.bfloat = bfloat;
-  rw.codes = reinterpret_cast<int8_t*>(wb + W.rawc);
-  rw.sT = reinterpret_cast<int16_t*>(wb + W.rawe);
-  int rc = launch_rows_prep(rw, stream);
-  if (rc) return rc;
-  const int64_t pcols = (int64_t)W.G * W.NB32 * 32;
-  hipLaunchKernelGGL(linear_pack_kernel, dim3((unsigned)((pcols * W.nbk + 255) / 256)), dim3(256), 0, stream,
-                     rw.codes, rw.sT, out_features, group_width, W.NB32, W.nbk, W.Cpad, pcols,
-                     reinterpret_cast<int8_t*>(wb + W.pk), reinterpret_cast<int16_t*>(wb + W.pe));
-  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL(linear_stats_kernel, dim3((unsigned)((pcols + 255) / 256)), dim3(256), 0, stream,
-                     reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps));
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-
 extern "C" int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* xq) {
   if (!p || !xq || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0 || xq->C <= 0) return -1;
   return attn_layout(p, score_mode(p, p->top_k || p->pred_out), xq).total;
@@ -686,34 +429,6 @@ extern "C" int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_p
                                        int32_t iters, float* stage_ms) {
   if (!xq) return MXA_ERR_ARG;
   return timed_impl(p, xq, stream, iters, stage_ms);
-}
-
-// ---- standalone top-k: one DPP row per row (mxa_topk_grp.hpp) -----------------------
-template <int NP>
-static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t stream) {
-  const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_grp_kernel<NP>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL(topk_grp_kernel<NP>, dim3(grid), dim3(256), lds, stream, ga);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-
-extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
-                        float* out_vals, uint32_t* out_mask, hipStream_t stream) {
-  if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
-  if (n > 512) return MXA_ERR_UNSUPPORTED;
-  if (rows == 0) return MXA_OK;
-  if (k == 0) {
-    if (out_mask) return hipMemsetAsync(out_mask, 0, (size_t)rows * ((n + 31) / 32) * 4, stream) == hipSuccess
-                             ? MXA_OK : MXA_ERR_LAUNCH;
-    return MXA_OK;
-  }
-  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask};
-  const unsigned grid = (unsigned)((rows + 15) / 16);
-  if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
-  if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);
-  return launch_topk_grp<512>(ga, grid, stream);
 }
 
 extern "C" int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc) {

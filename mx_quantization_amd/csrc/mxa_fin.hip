@@ -1,0 +1,138 @@
+// Row-kernel launches: the finishing kernel of the top-k path (mxa_finish.hpp) and the
+// dense (top_k=False) row kernel (mxa_rows2.hpp).
+#include <algorithm>
+
+#include "mxa_finish.hpp"
+#include "mxa_launch.hpp"
+
+namespace mxa {
+
+// ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
+static size_t rows2_total(const Rows2Args& ra, int W) {
+  return rows2_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.tpad, W).total;
+}
+// waves per workgroup: the size (8 or 16) that keeps the most waves resident per CU
+// (LDS-limited workgroups x waves, capped by the kernel's 7-waves-per-SIMD register use)
+static int rows2_waves(const Rows2Args& ra) {
+  auto resident = [&](int w) {
+    const size_t t = rows2_total(ra, w);
+    return t > 160 * 1024 ? 0 : std::min((int)(160 * 1024 / t) * w, 28);
+  };
+  const int r8 = resident(8), r16 = resident(16);
+  if (r8 > 0 || r16 > 0) return r16 > r8 ? 16 : 8;
+  return rows2_total(ra, 4) <= 160 * 1024 ? 4 : 0;
+}
+
+template <int S>
+static int launch_dense_s(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
+  Rows2Args ra = ra0;
+  ra.waves = rows2_waves(ra);
+  if (ra.waves <= 0) return MXA_ERR_UNSUPPORTED;
+  if (plan) return MXA_OK;
+  const size_t lds = rows2_total(ra, ra.waves);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&dense_rows_kernel<S>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  // few heads: split each head's rows over grid.y so that the launch still has ~4
+  // workgroups per CU
+  const int chunks = std::max(1, std::min((ra.N + ra.waves - 1) / ra.waves, 1024 / std::max(BH, 1)));
+  ra.rows_per_wg = (ra.N + chunks - 1) / chunks;
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL(dense_rows_kernel<S>, dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+// ---- finishing kernel (mxa_finish.hpp): 32-row MFMA tiles, one per wave ------------
+// two lanes per query row (one pass per tile) when every row's kept keys fit 2 x 16 slots
+static bool finish_pair(const Rows2Args& ra) { return ra.k_top <= 32; }
+static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg) {
+  const int tiles = (ra.N + kFinTile - 1) / kFinTile;
+  const bool pair = finish_pair(ra);
+  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, pair).total; };
+  if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  // a head's tiles round-robin over the waves of one workgroup (the K / V tables
+  // staged once per head); few heads (PixArt cross-attention): the tiles split over
+  // grid.y so that the grid still has ~2 workgroups per CU
+  int chunks = 1;
+  while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
+  // waves per workgroup: the fewest sequential tile rounds per CU -- workgroups per
+  // CU over the LDS-limited concurrency, times each workgroup's rounds over its
+  // tiles; ties to the smaller workgroup (measured: DeiT-base 4 waves, 2 workgroups
+  // per CU, 0.29 ms vs 0.36 ms with 5; DiT 8 waves, 0.36 ms vs 0.61 ms with 4)
+  const int tpc = (tiles + chunks - 1) / chunks;
+  const int64_t wgs_per_cu = ((int64_t)BH * chunks + 255) / 256;
+  int w = 1;
+  int64_t best = -1;
+  for (int c = 1; c <= std::min(8, tpc); ++c) {
+    const size_t t = lds(c);
+    if (t > 160 * 1024) break;
+    const int64_t conc = std::min<int64_t>(160 * 1024 / t, 12 / c > 0 ? 12 / c : 1);
+    const int64_t score = (wgs_per_cu + conc - 1) / conc * ((tpc + c - 1) / c);
+    if (best < 0 || score < best) best = score, w = c;
+  }
+  *waves = w;
+  *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
+  return MXA_OK;
+}
+template <int NB, int KS, bool PAIR>
+static int launch_finish_ks(const Rows2Args& ra0, int BH, hipStream_t stream) {
+  Rows2Args ra = ra0;
+  int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
+  if (rc) return rc;
+  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NB>
+static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (finish_pair(ra)) {  // slots per lane: ceil(k / 2)
+    const int kp = (ra.k_top + 1) / 2;
+    if (kp <= 2) return launch_finish_ks<NB, 2, true>(ra, BH, stream);
+    if (kp <= 4) return launch_finish_ks<NB, 4, true>(ra, BH, stream);
+    if (kp <= 8) return launch_finish_ks<NB, 8, true>(ra, BH, stream);
+    if (kp <= 12) return launch_finish_ks<NB, 12, true>(ra, BH, stream);
+    return launch_finish_ks<NB, 16, true>(ra, BH, stream);
+  }
+  const int ks = (ra.k_top + 15) / 16;
+  if (ks <= 1) return launch_finish_ks<NB, 1, false>(ra, BH, stream);
+  if (ks <= 2) return launch_finish_ks<NB, 2, false>(ra, BH, stream);
+  if (ks <= 4) return launch_finish_ks<NB, 4, false>(ra, BH, stream);
+  if (ks <= 8) return launch_finish_ks<NB, 8, false>(ra, BH, stream);
+  if (ks <= 16) return launch_finish_ks<NB, 16, false>(ra, BH, stream);
+  return launch_finish_ks<NB, 32, false>(ra, BH, stream);
+}
+static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (plan) {
+    int w, r;
+    return finish_plan(ra, BH, &w, &r);
+  }
+  switch (ra.nbd) {
+    case 1: return launch_finish_nb<1>(ra, BH, stream);
+    case 2: return launch_finish_nb<2>(ra, BH, stream);
+    case 3: return launch_finish_nb<3>(ra, BH, stream);
+    default: return launch_finish_nb<4>(ra, BH, stream);
+  }
+}
+
+// the row kernel of the path: the finishing kernel (top-k) or the dense kernel
+int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan) {
+  if (topk) {
+    // the selection kernel already wrote the true scores when it ranked them
+    Rows2Args rf = ra;
+    if (true_mode) rf.true_out = nullptr;
+    return launch_finish(rf, BH, stream, plan);
+  }
+  switch (S) {
+    case 1: return launch_dense_s<1>(ra, BH, stream, plan);
+    case 2: return launch_dense_s<2>(ra, BH, stream, plan);
+    case 4: return launch_dense_s<4>(ra, BH, stream, plan);
+    default: return launch_dense_s<8>(ra, BH, stream, plan);
+  }
+}
+
+
+}  // namespace mxa

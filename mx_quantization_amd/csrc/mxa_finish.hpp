@@ -354,23 +354,4 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   }
 }
 
-// Self-test of the v_mfma_i32_32x32x32_i8 lane maps used above: A (32x32 row-major
-// M x K), B (32x32 row-major K x N) -> C (32x32 row-major) through the same maps.
-__global__ void selftest_mfma32_kernel(const int8_t* A, const int8_t* B, int32_t* C) {
-  const int lane = threadIdx.x, ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
-  v4i_ a4, b4;
-  for (int w = 0; w < 4; ++w) {
-    uint32_t x = 0, y = 0;
-    for (int j = 0; j < 4; ++j) {
-      x |= (uint32_t)(uint8_t)A[ln * 32 + kh + 4 * w + j] << (8 * j);
-      y |= (uint32_t)(uint8_t)B[(kh + 4 * w + j) * 32 + ln] << (8 * j);
-    }
-    a4[w] = (int)x;
-    b4[w] = (int)y;
-  }
-  const v16i zero = {};
-  const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a4, b4, zero, 0, 0, 0);
-  for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + m0 + (i & 3)) * 32 + ln] = c[i];
-}
-
 }  // namespace mxa

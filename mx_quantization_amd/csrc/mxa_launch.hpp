@@ -1,0 +1,20 @@
+// Host-side launchers shared across the library's translation units (one TU per
+// kernel family, so that hipcc compiles them in parallel).
+#pragma once
+#include "mxa_proj_args.hpp"
+#include "mxa_rows2.hpp"
+
+namespace mxa {
+
+inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+// selection kernel (mxa_sel.hip); plan: only check the LDS budget, launch nothing
+int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);
+int launch_select_p1(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);  // OpExp, OpMul
+int launch_select_p2(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);  // TrueEx, Elsa, True
+// the row kernel of the path: finishing kernel (top-k) or dense row kernel (mxa_fin.hip)
+int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan);
+// fused qkv projection kernel (mxa_proj.hip)
+int launch_proj(const ProjArgs& pa, hipStream_t stream);
+
+}  // namespace mxa

@@ -20,102 +20,11 @@
 
 #include "mxa_finish.hpp"
 #include "mxa_prep.hpp"
+#include "mxa_proj_args.hpp"
 
 namespace mxa {
 
-// Prepared Linear weight (mxa_linear_weight_prep): output columns in groups of gw (a
-// head's q, k or v: gw = D), each group padded to NB32 = ceil(gw/32) 32-column blocks.
-//   pk  MFMA-ready codes [group][cb][kb][lane 0..63][16 B]: lane = n + 32 h holds
-//       W[col n][32 kb + 16 h .. + 16] -- one coalesced 1-KB load per wave and K-block
-//   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
-//   ps  per padded column: smallest finite block exponent, spread (int16 pair)
-//   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
-struct LinearLayout {
-  int G, NB32, nbk, Cpad;
-  int64_t pk, pe, ps, rawc, rawe, total;
-};
-__host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int gw) {
-  LinearLayout L;
-  auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
-  L.G = out_f / gw;
-  L.NB32 = (gw + 31) / 32;
-  L.nbk = (in_f + 31) / 32;
-  L.Cpad = 32 * L.nbk;
-  const int64_t pcols = (int64_t)L.G * L.NB32 * 32;
-  int64_t o = 0;
-  L.pk = o;
-  o += al(pcols * L.Cpad);
-  L.pe = o;
-  o += al(pcols * L.nbk * 2);
-  L.ps = o;
-  o += al(pcols * 4);
-  L.rawc = o;
-  o += al((int64_t)out_f * L.Cpad);
-  L.rawe = o;
-  o += al((int64_t)out_f * L.nbk * 2);
-  L.total = o;
-  return L;
-}
 
-// one thread per (padded column, K-block): the MFMA-ready codes and the exponents
-__global__ __launch_bounds__(256) void linear_pack_kernel(const int8_t* rawc, const int16_t* rawe, int out_f, int gw,
-                                                          int NB32, int nbk, int Cpad, int64_t pcols, int8_t* pk,
-                                                          int16_t* pe) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= pcols * nbk) return;
-  const int64_t pc = t / nbk;
-  const int kb = (int)(t - pc * nbk);
-  const int64_t blkc = pc / 32;  // group * NB32 + cb
-  const int n = (int)(pc - blkc * 32);
-  const int64_t g = blkc / NB32;
-  const int cb = (int)(blkc - g * NB32);
-  const int gc = 32 * cb + n;
-  const bool real = gc < gw;
-  const int64_t col = g * gw + gc;
-  uint4 lo = make_uint4(0, 0, 0, 0), hi = make_uint4(0, 0, 0, 0);
-  int16_t e = 0;
-  if (real) {
-    lo = *reinterpret_cast<const uint4*>(rawc + col * Cpad + 32 * kb);
-    hi = *reinterpret_cast<const uint4*>(rawc + col * Cpad + 32 * kb + 16);
-    e = rawe[col * nbk + kb];
-  }
-  int8_t* dst = pk + ((blkc * nbk + kb) * 64) * 16;
-  *reinterpret_cast<uint4*>(dst + n * 16) = lo;
-  *reinterpret_cast<uint4*>(dst + (n + 32) * 16) = hi;
-  pe[pc * nbk + kb] = e;
-}
-
-// per padded column: smallest finite block exponent and the spread
-__global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, int64_t pcols, int nbk, int16_t* ps) {
-  const int64_t pc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (pc >= pcols) return;
-  int lo = 1 << 20, hi = -(1 << 20);
-  for (int kb = 0; kb < nbk; ++kb) {
-    const int e = exp_from16(pe[pc * nbk + kb]);
-    if (e != kExpNaN) {
-      lo = min(lo, e);
-      hi = max(hi, e);
-    }
-  }
-  if (lo > hi) lo = hi = 0;
-  ps[2 * pc] = (int16_t)lo;
-  ps[2 * pc + 1] = (int16_t)(hi - lo);
-}
-
-struct ProjArgs {
-  const int8_t* xc;   // x codes [B*N][Cpad]
-  const int16_t* xs;  // x code-unit exponents [B*N][nbk]
-  const int8_t* pk;   // prepared weight (LinearLayout with gw = D)
-  const int16_t* pe;
-  const int16_t* ps;
-  const float* bias;  // [3*H*D] or null
-  float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
-  int B, N, H, D, nbk, Cpad, bfloat;
-  int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
-  int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
-  RowsPrepArgs rq, rk;  // q / k row outputs (rows_prep layout)
-  ColsPrepArgs cv;      // V outputs (cols_prep layout)
-};
 
 struct ProjLds {
   size_t xt, xe, rlo, rhi, rn, st, ot, total;

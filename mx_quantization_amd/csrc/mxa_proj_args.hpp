@@ -1,0 +1,56 @@
+// Argument block and prepared-weight layout of the fused qkv projection (mxa_proj.hpp).
+#pragma once
+#include "mxa_kernels.hpp"
+
+namespace mxa {
+
+// Prepared Linear weight (mxa_linear_weight_prep): output columns in groups of gw (a
+// head's q, k or v: gw = D), each group padded to NB32 = ceil(gw/32) 32-column blocks.
+//   pk  MFMA-ready codes [group][cb][kb][lane 0..63][16 B]: lane = n + 32 h holds
+//       W[col n][32 kb + 16 h .. + 16] -- one coalesced 1-KB load per wave and K-block
+//   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
+//   ps  per padded column: smallest finite block exponent, spread (int16 pair)
+//   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
+struct LinearLayout {
+  int G, NB32, nbk, Cpad;
+  int64_t pk, pe, ps, rawc, rawe, total;
+};
+__host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int gw) {
+  LinearLayout L;
+  auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+  L.G = out_f / gw;
+  L.NB32 = (gw + 31) / 32;
+  L.nbk = (in_f + 31) / 32;
+  L.Cpad = 32 * L.nbk;
+  const int64_t pcols = (int64_t)L.G * L.NB32 * 32;
+  int64_t o = 0;
+  L.pk = o;
+  o += al(pcols * L.Cpad);
+  L.pe = o;
+  o += al(pcols * L.nbk * 2);
+  L.ps = o;
+  o += al(pcols * 4);
+  L.rawc = o;
+  o += al((int64_t)out_f * L.Cpad);
+  L.rawe = o;
+  o += al((int64_t)out_f * L.nbk * 2);
+  L.total = o;
+  return L;
+}
+
+struct ProjArgs {
+  const int8_t* xc;   // x codes [B*N][Cpad]
+  const int16_t* xs;  // x code-unit exponents [B*N][nbk]
+  const int8_t* pk;   // prepared weight (LinearLayout with gw = D)
+  const int16_t* pe;
+  const int16_t* ps;
+  const float* bias;  // [3*H*D] or null
+  float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
+  int B, N, H, D, nbk, Cpad, bfloat;
+  int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
+  int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
+  RowsPrepArgs rq, rk;  // q / k row outputs (rows_prep layout)
+  ColsPrepArgs cv;      // V outputs (cols_prep layout)
+};
+
+}  // namespace mxa

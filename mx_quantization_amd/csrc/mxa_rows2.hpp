@@ -10,7 +10,7 @@
 // workloads/PixArt/models/MX_transformer_block.py:648-717, :792-859; the MX matmul
 // of P.V: microxscaling/mx/matmul.py:68-76.
 #pragma once
-#include "mxa_order.hpp"
+#include "mxa_modes.hpp"
 
 namespace mxa {
 

@@ -1,0 +1,103 @@
+// Selection kernel launches (mxa_select.hpp): the attention path's approximate scores +
+// exact-order top-k, and the standalone mxa_topk entry point of include/mxa.h.
+#include "mxa_launch.hpp"
+#include "mxa_select.hpp"
+
+namespace mxa {
+
+// ---- selection kernel (mxa_select.hpp): four query rows per wave -------------------
+template <int NP, int MODE, int W>
+static size_t select_lds(const Rows2Args& ra) {
+  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP);
+}
+template <int NP, int MODE, int W>
+static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
+  Rows2Args ra = ra0;
+  const size_t lds = select_lds<NP, MODE, W>(ra);
+  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  if (plan) return MXA_OK;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
+  int rows = kSelRows;
+  while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
+  ra.rows_per_wg = rows;
+  const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
+  hipLaunchKernelGGL((select_kernel<NP, MODE, W>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NP, int MODE>
+static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
+  return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
+}
+template <int MODE>
+static int launch_select_m(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (ra.T <= 128) return launch_select_np<128, MODE>(ra, BH, stream, plan);
+  if (ra.T <= 256) return launch_select_np<256, MODE>(ra, BH, stream, plan);
+  return launch_select_np<512, MODE>(ra, BH, stream, plan);
+}
+// The selection kernel's instantiations are split over three compilations of this
+// file (MXA_SEL_PART 0, 1, 2: build_native.py) so that hipcc builds them in parallel.
+#ifndef MXA_SEL_PART
+#define MXA_SEL_PART 0
+#endif
+#if MXA_SEL_PART == 0
+int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
+  switch (mode) {
+    case kModeExSign: return launch_select_m<kModeExSign>(ra, BH, stream, plan);
+    case kModeOpExp:
+    case kModeOpMul: return launch_select_p1(ra, mode, BH, stream, plan);
+    default: return launch_select_p2(ra, mode, BH, stream, plan);
+  }
+}
+#elif MXA_SEL_PART == 1
+int launch_select_p1(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
+  return mode == kModeOpMul ? launch_select_m<kModeOpMul>(ra, BH, stream, plan)
+                            : launch_select_m<kModeOpExp>(ra, BH, stream, plan);
+}
+#else
+int launch_select_p2(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
+  switch (mode) {
+    case kModeTrueEx: return launch_select_m<kModeTrueEx>(ra, BH, stream, plan);
+    case kModeElsa: return launch_select_m<kModeElsa>(ra, BH, stream, plan);
+    default: return launch_select_m<kModeTrue>(ra, BH, stream, plan);
+  }
+}
+#endif
+
+}  // namespace mxa
+
+#if MXA_SEL_PART == 0
+using namespace mxa;
+
+// ---- standalone top-k: one DPP row per row (mxa_topk_grp.hpp) -----------------------
+template <int NP>
+static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t stream) {
+  const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_grp_kernel<NP>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL(topk_grp_kernel<NP>, dim3(grid), dim3(256), lds, stream, ga);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
+                        float* out_vals, uint32_t* out_mask, hipStream_t stream) {
+  if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
+  if (n > 512) return MXA_ERR_UNSUPPORTED;
+  if (rows == 0) return MXA_OK;
+  if (k == 0) {
+    if (out_mask) return hipMemsetAsync(out_mask, 0, (size_t)rows * ((n + 31) / 32) * 4, stream) == hipSuccess
+                             ? MXA_OK : MXA_ERR_LAUNCH;
+    return MXA_OK;
+  }
+  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask};
+  const unsigned grid = (unsigned)((rows + 15) / 16);
+  if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
+  if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);
+  return launch_topk_grp<512>(ga, grid, stream);
+}
+
+#endif  // MXA_SEL_PART == 0

@@ -21,6 +21,7 @@
 //   workloads/PixArt/models/MX_transformer_block.py:656-678, :805-825.
 #pragma once
 #include <type_traits>
+#include "mxa_rows2.hpp"
 #include "mxa_topk_grp.hpp"
 
 namespace mxa {
