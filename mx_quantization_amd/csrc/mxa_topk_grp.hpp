@@ -93,6 +93,23 @@ __device__ __forceinline__ uint32_t g_shl_le(uint32_t acc, uint32_t a, uint32_t 
   asm("v_cmp_le_u32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
   return acc;
 }
+// the stop masks of two positions at once: L = 4 L + 2 (k0 <= p) + (k1 <= p),
+// R = 4 R + 2 (p <= k0) + (p <= k1).  The four compares go to four SGPR pairs first,
+// so each add-with-carry reads a carry written three instructions earlier: no wait
+// states (one compare + add-with-carry pair at a time needs an s_nop between them)
+__device__ __forceinline__ void g_stops2(uint32_t& L, uint32_t& R, uint32_t k0, uint32_t k1, uint32_t p) {
+  uint64_t c0, c1, c2, c3;
+  asm("v_cmp_le_u32_e64 %2, %6, %8\n\t"
+      "v_cmp_le_u32_e64 %3, %8, %6\n\t"
+      "v_cmp_le_u32_e64 %4, %7, %8\n\t"
+      "v_cmp_le_u32_e64 %5, %8, %7\n\t"
+      "v_addc_co_u32_e64 %0, %2, %0, %0, %2\n\t"
+      "v_addc_co_u32_e64 %1, %3, %1, %1, %3\n\t"
+      "v_addc_co_u32_e64 %0, %4, %0, %0, %4\n\t"
+      "v_addc_co_u32_e64 %1, %5, %1, %1, %5"
+      : "+v"(L), "+v"(R), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+      : "v"(k0), "v"(k1), "v"(p));
+}
 
 // r + (a > b) for 64-bit a, b: a compare and an add-with-carry
 __device__ __forceinline__ uint32_t g_add_gt(uint32_t r, uint64_t a, uint64_t b) {
@@ -138,38 +155,48 @@ constexpr int pow2_floor() { return E >= 32 ? 32 : E >= 16 ? 16 : E >= 8 ? 8 : E
 // HP = NP / 2 (>= any swap count).  Returns the cut.
 template <int E, int NP>
 __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
+  static_assert(E % 2 == 0, "window widths are even");
   constexpr int HP = NP / 2;
   const int fa = act ? f : 0, la = act ? l : 4;  // idle rows read harmless positions
   const int mid = fa + (int)((uint32_t)(la - fa) >> 1);
-  const lu32* A32 = (const lu32*)g.A;  // the keys alone (32-bit compares)
-  const uint32_t ka = A32[2 * fa + 3], kb = A32[2 * mid + 1], kc = A32[2 * la - 1];
-  // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free
-  const bool ab = ka > kb, bc = kb > kc, ac = ka > kc;
-  const int m = ab ? (bc ? mid : (ac ? la - 1 : fa + 1)) : (ac ? fa + 1 : (bc ? la - 1 : mid));
-  const uint64_t xm = g.A[m], xf = g.A[fa];
-  const uint32_t p = hi32(xm);
+  const int lb = b + E * gl;
+  // the median candidates (whole elements) and the window, all in one LDS round trip:
+  // the median's iter_swap is applied to the stop masks in registers and written back
+  // while the masks are formed (position f is never a stop; position m holds old f)
+  const uint64_t xf = g.A[fa], xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1];
+  uint32_t K[E];
+#pragma unroll
+  for (int e = 0; e < E; e += 2) {
+    const u32x4 v = *(const lu128*)(g.A + lb + e);
+    K[e] = v.y;
+    K[e + 1] = v.w;
+  }
+  const uint32_t ka = hi32(xa), kb = hi32(xb), kc = hi32(xc);
+  // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free:
+  //   a>b: (b>c ? mid : a>c ? l-1 : f+1);  else: (a>c ? f+1 : b>c ? l-1 : mid)
+  const uint32_t ab = ka > kb, bc = kb > kc, ac = ka > kc;
+  const uint32_t pick_b = (ab & bc) | (~ab & ~ac & ~bc & 1u);
+  const uint32_t pick_c = (ab & ~bc & ac) | (~ab & ~ac & bc & 1u);
+  int m = fa + 1;
+  uint64_t xm = xa;
+  m = pick_c ? la - 1 : m;
+  xm = pick_c ? xc : xm;
+  m = pick_b ? mid : m;
+  xm = pick_b ? xb : xm;
+  const uint32_t p = hi32(xm), kf = hi32(xf);
   if (act) {  // iter_swap(f, median)
     g.A[f] = xm;
     g.A[m] = xf;
   }
-  wave_lds_sync();
-
-  const int lb = b + E * gl;
-  uint32_t K[E], I[E];
-#pragma unroll
-  for (int e = 0; e < E; e += 2) {
-    const u32x4 v = *(const lu128*)(g.A + lb + e);
-    I[e] = v.x;
-    K[e] = v.y;
-    I[e + 1] = v.z;
-    K[e + 1] = v.w;
-  }
   // stop masks, bit (E-1-e) <-> position lb + e
   uint32_t Lm = 0, Rm = 0;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    Lm = g_shl_le(Lm, K[e], p);  // left stop:  !(a > p)
-    Rm = g_shl_le(Rm, p, K[e]);  // right stop: !(p > a)
+  for (int e = 0; e < E; e += 2) g_stops2(Lm, Rm, K[e], K[e + 1], p);
+  {  // position m now holds old f (key kf)
+    const int em = m - lb;
+    const uint32_t bm = (uint32_t)em < (uint32_t)E ? 1u << (E - 1 - em) : 0u;
+    Lm = (Lm & ~bm) | (kf <= p ? bm : 0u);
+    Rm = (Rm & ~bm) | (p <= kf ? bm : 0u);
   }
   const int lo = min(max(f + 1 - lb, 0), E), hi = min(max(l - lb, 0), E);
   const uint32_t rng = act ? (lowbits(E - lo) & ~lowbits(E - hi)) : 0u;
@@ -188,16 +215,17 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
     const bool ok = c <= E && PLR + (uint32_t)__popc(Lm >> sh) + (uint32_t)__popc(Rm >> sh) <= totR;
     j = ok ? c : j;
   }
-  const int cut = b + (int)g_sum((uint32_t)j);
-  // swapping left stops: the left stops below the cut (nsw of them, left ranks
-  // 0 .. nsw-1); swapping right stops: the nsw highest (ranks from the top 0 .. nsw-1)
-  const int cl = min(max(cut - lb, 0), E);
-  const uint32_t SLm = Lm & ~lowbits(E - cl);
-  const uint32_t nsw = g_sum((uint32_t)__popc(SLm));
+  // the swapping left stops are the left stops below the cut: in this lane the left
+  // stops of its first j positions.  One scan gives the cut and their count nsw.
+  const uint32_t SLm = Lm & ~lowbits(E - j);
+  const uint32_t cj = (uint32_t)j | ((uint32_t)__popc(SLm) << 16);
+  const uint32_t sums = g_sum(cj);
+  const int cut = b + (int)(sums & 0xFFFFu);
+  const uint32_t nsw = sums >> 16;
   // the exchange: every swapping left stop publishes its position at HP + its rank,
-  // every swapping right stop at its rank from the top, the rest at the lane's trash
-  // slot; then the t-th pairs trade elements, 16 pairs a row at a time (only the
-  // swaps move: ~range/4 of the positions)
+  // every swapping right stop (the nsw highest right stops) at its rank from the top,
+  // the rest at the lane's trash slot; then the t-th pairs trade elements, 16 pairs a
+  // row at a time (only the swaps move: ~range/4 of the positions)
   // (u8 slots: the slot values are LDS byte addresses, the base folded into the
   // popcount accumulations)
   const uint32_t ob = NP <= 256 ? (uint32_t)(size_t)g.P : 0u;
@@ -207,7 +235,10 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
     const int sh = E - 1 - e;
     const uint32_t tl = lbase + (uint32_t)__popc((Lm >> sh) >> 1);
     const uint32_t tr = rbase - (uint32_t)__popc(Rm >> sh);
-    const uint32_t slot = ((SLm >> sh) & 1u) ? tl : (((Rm >> sh) & 1u) && tr < rlim ? tr : trash);
+    // branch-free: slot = swapping left stop ? tl : (swapping right stop ? tr : trash)
+    const uint32_t rsw = ((Rm >> sh) & 1u) & (uint32_t)(tr < rlim);
+    uint32_t slot = rsw ? tr : trash;
+    slot = ((SLm >> sh) & 1u) ? tl : slot;
     if constexpr (NP <= 256) *(lu8*)(size_t)slot = (uint8_t)(lb + e);
     else p_put<NP>(g, slot, (uint32_t)(lb + e));
   }
