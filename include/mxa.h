@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MXA_ABI_VERSION 2
+#define MXA_ABI_VERSION 3
 
 /* status codes */
 #define MXA_OK 0
@@ -31,6 +31,15 @@ extern "C" {
 #define MXA_ERR_UNSUPPORTED (-2)  /* valid for the reference, not implemented here */
 #define MXA_ERR_LAUNCH (-3)       /* HIP launch error */
 #define MXA_ERR_WORKSPACE (-4)    /* workspace too small */
+
+/* storage dtypes of tensor arguments.  The reference's ops follow their input's dtype
+ * (microxscaling/mx/mx_ops.py:85, :283; elemwise_ops.py:146): on float16 / bfloat16
+ * tensors the shared exponent is floor(log2) computed in that dtype, a float16 all-zero
+ * block quantizes to NaN (2^-126 underflows: log2(0) = -inf, scale 2^-127 = 0, 0/0),
+ * and every op's result is a tensor of that dtype. */
+#define MXA_DT_F32 0
+#define MXA_DT_F16 1
+#define MXA_DT_BF16 2
 
 /* rounding modes: microxscaling/mx/formats.py:12-16 (RoundingMode) */
 #define MXA_ROUND_NEAREST 0
@@ -71,37 +80,38 @@ const char* mxa_status_string(int status);
  *   codes  : element codes, same layout as x (nullable)
  *   exps   : block scale exponents (outer, nblocks, inner), INT16_MIN = NaN (nullable)
  *   bfloat : elementwise pre-rounding of x (0/32 = none, 16 = bfloat16; quantize_elemwise_op)
+ *   dtype  : MXA_DT_* of x and y
  */
-int mxa_quantize_mx(const float* x, float* y, int8_t* codes, int16_t* exps,
+int mxa_quantize_mx(const void* x, void* y, int8_t* codes, int16_t* exps,
                     int64_t outer, int64_t axis_len, int64_t inner, int32_t block_size,
                     int32_t elem_mbits, int32_t scale_bits, int32_t round_mode,
-                    int32_t flush_subnormals, int32_t bfloat, hipStream_t stream);
+                    int32_t flush_subnormals, int32_t bfloat, int32_t dtype, hipStream_t stream);
 
 /*
  * Shared exponents of the blocks of a (outer, axis_len, inner) tensor.
  * Replaces _shared_exponents (microxscaling/mx/mx_ops.py:49-99).
  *   method 0 = "max" -> out (outer, nblocks, inner); 1 = "none" -> out like x.
- *   ebits > 0 applies the [-emax, emax] / NaN clamp of :90-97.
+ *   ebits > 0 applies the [-emax, emax] / NaN clamp of :90-97.  x and out: dtype (MXA_DT_*).
  */
-int mxa_shared_exponents(const float* x, float* out, int64_t outer, int64_t axis_len, int64_t inner,
-                         int32_t block_size, int32_t method, int32_t ebits, hipStream_t stream);
+int mxa_shared_exponents(const void* x, void* out, int64_t outer, int64_t axis_len, int64_t inner,
+                         int32_t block_size, int32_t method, int32_t ebits, int32_t dtype, hipStream_t stream);
 
 /*
  * Elementwise bfloatX quantization.  Replaces quantize_elemwise_op / _quantize_bfloat
  * (microxscaling/mx/elemwise_ops.py:201-277) and quantize_elemwise_func_cuda
  * (microxscaling/mx/cpp/elemwise.cu:12-95).
  */
-int mxa_quantize_bfloat(const float* x, float* y, int64_t n, int32_t bfloat, int32_t round_mode,
-                        int32_t allow_denorm, hipStream_t stream);
+int mxa_quantize_bfloat(const void* x, void* y, int64_t n, int32_t bfloat, int32_t round_mode,
+                        int32_t allow_denorm, int32_t dtype, hipStream_t stream);
 
 /*
  * Approximator operand values along the last axis (rows x d, leading dims ld_x / ld_out),
  * MX block size 32.  Replaces the tensors returned by exponent_approximation's methods
- * (funcs/exponent_based_prediction.py:44-318): op_kind MXA_OP_*.
+ * (funcs/exponent_based_prediction.py:44-318): op_kind MXA_OP_*.  x and out: dtype.
  */
-int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64_t ld_x,
+int mxa_approx_values(const void* x, void* out, int64_t rows, int32_t d, int64_t ld_x,
                       int64_t ld_out, int32_t op_kind, int32_t flush_subnormals, int32_t bfloat,
-                      hipStream_t stream);
+                      int32_t dtype, hipStream_t stream);
 
 /*
  * torch.topk(vals, k, dim=-1, largest=True, sorted=True) with torch's CPU index
@@ -111,10 +121,10 @@ int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64
  * rows x n float32 with leading dim ld; n <= 512.  out_vals nullable.
  * out_mask (nullable): the prune mask zeros.scatter_(-1, idx, 1) of the callers
  * (deit main.py:147-148; examples/deit/top_k.py:16-42) as rows x ceil(n/32)
- * words, bit j%32 of word j/32 set iff j is kept.
+ * words, bit j%32 of word j/32 set iff j is kept.  vals / out_vals: dtype (MXA_DT_*).
  */
-int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
-             int64_t* out_idx, float* out_vals, uint32_t* out_mask, hipStream_t stream);
+int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
+             int64_t* out_idx, void* out_vals, uint32_t* out_mask, int32_t dtype, hipStream_t stream);
 
 /*
  * The fused hot path: MXINT8 true scores, approximate scores, top-k prune,
@@ -127,9 +137,9 @@ int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
  * Strides are in elements for the (b,h,row) dims; the D dim must be contiguous.
  */
 typedef struct mxa_attn_params {
-  const float* q;
-  const float* k;
-  const float* v;
+  const void* q;           /* dtype `dtype`                                                 */
+  const void* k;
+  const void* v;
   int64_t q_strides[3];
   int64_t k_strides[3];
   int64_t v_strides[3];
@@ -141,9 +151,9 @@ typedef struct mxa_attn_params {
   int32_t approx;          /* 0: top-k on the true scores (approx_flag / ex_pred False)    */
   int32_t flush_subnormals;/* mx_specs["mx_flush_fp32_subnorms"]                           */
   int32_t bfloat;          /* mx_specs["bfloat"]: 0/32 none, 16 bfloat16                   */
-  const float* bias;       /* additive score bias (PixArt mask), nullable                 */
+  const void* bias;        /* additive score bias (PixArt mask), dtype `dtype`, nullable   */
   int64_t bias_strides[4]; /* (b,h,n,t) element strides, 0 = broadcast                     */
-  float* out;              /* (B,H,N,D) output                                             */
+  void* out;               /* (B,H,N,D) output, dtype: score_dtype ? score_dtype : dtype   */
   int64_t out_strides[3];
   int64_t* idx_out;        /* (B,H,N,k_top) contiguous int64, nullable                     */
   float* true_out;         /* optional (B,H,N,T) contiguous true scores (tests)            */
@@ -157,6 +167,13 @@ typedef struct mxa_attn_params {
                               device, correctly rounded                                    */
   void* workspace;         /* device scratch of mxa_attention_workspace_bytes() bytes     */
   int64_t workspace_bytes;
+  int32_t dtype;           /* MXA_DT_* of q, k, v, bias: their MX quantization follows it   */
+  int32_t score_dtype;     /* 0: the GEMM outputs (true / approximate scores, P, out) are in
+                              `dtype` (the ops on tensors of that dtype); MXA_DT_F16 / BF16:
+                              torch.autocast -- the fp32 q, k, v operands' matmuls return that
+                              dtype, P = zeros_like(true scores) is of it and is quantized by its
+                              rules (deit main.py:101, :118, :147; engine.py:97).  true_out /
+                              pred_out hold those dtype values as float32.                  */
 } mxa_attn_params;
 
 int64_t mxa_attention_workspace_bytes(const mxa_attn_params* p);
@@ -218,6 +235,9 @@ typedef struct mxa_qkv_params {
   const void* wq;        /* mxa_linear_weight_prep output for W (3*H*D, C), group_width D    */
   const float* bias;     /* (3*H*D) or null                                                 */
   float* qkv_out;        /* optional (B*N, 3*H*D) fp32 projection (tests)                   */
+  int32_t autocast_dtype;/* 0, or MXA_DT_F16 / BF16: torch.autocast's F.linear -- the product
+                            rounded to that dtype, then + bias in fp32 (linear.py:88-101 under
+                            autocast: the fp16 output + fp32 bias promotes to fp32)         */
 } mxa_qkv_params;
 
 int64_t mxa_linear_weight_bytes(int32_t out_features, int32_t in_features, int32_t group_width);
@@ -225,19 +245,22 @@ int mxa_linear_weight_prep(const float* w, int32_t out_features, int32_t in_feat
                            int32_t flush_subnormals, int32_t bfloat, void* wq, hipStream_t stream);
 int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* x);
 int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream);
-/* mxa_attention_timed for the fused projection path (stage 1 = x quantize + projection) */
+/* mxa_attention_timed for the fused projection path (stage 0 = x quantize + projection) */
 int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream, int32_t iters,
                             float* stage_ms);
 
 /*
  * mx.matmul forward (microxscaling/mx/matmul.py:31-100, :211-222): in1 (batch, M, K)
  * quantized along K, in2 (batch, K, Nc) quantized along K, fp32 result (batch, M, Nc)
- * contiguous.  Integer formats, block size 32.
+ * contiguous.  Integer formats, block size 32.  a_dtype / b_dtype (MXA_DT_*): each operand's
+ * MX quantization follows its dtype; c is the exact product rounded once to c_dtype (the
+ * operands' dtype, or torch.autocast's: P (float16) @ V (float32) under autocast, deit
+ * main.py:152 with engine.py:97).
  */
-int mxa_matmul(const float* a, const float* b, float* c, int64_t batch, int32_t M, int32_t K,
+int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, int32_t K,
                int32_t Nc, int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a,
-               int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, void* workspace,
-               int64_t workspace_bytes, hipStream_t stream);
+               int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype,
+               int32_t b_dtype, int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream);
 int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc);
 
 /* Self-tests of the int8 MFMA operand/accumulator lane maps the kernels rely on:

@@ -21,7 +21,9 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
-ABI_VERSION = 2
+ABI_VERSION = 3
+DT_F32, DT_F16, DT_BF16 = 0, 1, 2
+DTYPES = {torch.float32: DT_F32, torch.float16: DT_F16, torch.bfloat16: DT_BF16}
 PATH_NAMES = {2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
 PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4,
               "true_ex": 5, "ELSA": 6}
@@ -41,24 +43,25 @@ class AttnParams(ctypes.Structure):
         ("idx_out", c_vp), ("true_out", c_vp), ("pred_out", c_vp), ("mask_out", c_vp),
         ("elsa_proj", c_vp), ("elsa_cos", c_vp),
         ("workspace", c_vp), ("workspace_bytes", c_i64),
+        ("dtype", c_i32), ("score_dtype", c_i32),
     ]
 
 
 class QkvParams(ctypes.Structure):
     """mirror of struct mxa_qkv_params (include/mxa.h)"""
     _fields_ = [("x", c_vp), ("x_row_stride", c_i64), ("C", c_i32), ("wq", c_vp), ("bias", c_vp),
-                ("qkv_out", c_vp)]
+                ("qkv_out", c_vp), ("autocast_dtype", c_i32)]
 
 
 _SIGS = {
     "mxa_abi_version": (c_i32, []),
     "mxa_status_string": (ctypes.c_char_p, [c_i32]),
     "mxa_quantize_mx": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32,
-                                c_i32, c_vp]),
-    "mxa_shared_exponents": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
-    "mxa_quantize_bfloat": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
-    "mxa_approx_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
-    "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+                                c_i32, c_i32, c_vp]),
+    "mxa_shared_exponents": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_quantize_bfloat": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_approx_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp]),
+    "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "mxa_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams)]),
     "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
@@ -71,7 +74,7 @@ _SIGS = {
     "mxa_qkv_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp, c_i32,
                                         ctypes.POINTER(c_f32)]),
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
-                           c_vp, c_i64, c_vp]),
+                           c_i32, c_i32, c_i32, c_vp, c_i64, c_vp]),
     "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
     "mxa_selftest_mfma": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
     "mxa_selftest_mfma32": (c_i32, [c_vp, c_vp, c_vp, c_vp]),

@@ -50,8 +50,8 @@ struct MatmulArgs {
   const int16_t* as;
   const int8_t* bt;
   const int16_t* bsc;
-  int M, Nc, nbk, kpad, bfloat;
-  float* c;
+  int M, Nc, nbk, kpad, bfloat, dt;
+  void* c;  // dtype dt
 };
 
 __global__ __launch_bounds__(256) void matmul_kernel(MatmulArgs a) {
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void matmul_kernel(MatmulArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * (lane >> 4) + i;
     if (r < rows_valid && col < a.Nc)
-      a.c[(arow0 + r) * a.Nc + col] = round_bfloat((float)acc[i], a.bfloat, kRoundNearest, 1);
+      store_dt(a.c, (arow0 + r) * a.Nc + col, round_bfloat(round_dt((float)acc[i], a.dt), a.bfloat, kRoundNearest, 1, a.dt), a.dt);
   }
 }
 
@@ -195,7 +195,7 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   rx.x = xq.x; rx.s0 = 0; rx.s1 = 0; rx.s2 = xq.x_row_stride;
   rx.H = 1; rx.R = tokens; rx.rows = tokens; rx.D = xq.C; rx.nb = nbk; rx.dpad = Cpad;
   rx.vec4 = aligned16(xq.x) && xq.x_row_stride % 4 == 0;
-  rx.op_kind = MXA_OP_MXINT8; rx.flush = pp.flush_subnormals; rx.bfloat = pp.bfloat;
+  rx.op_kind = MXA_OP_MXINT8; rx.flush = pp.flush_subnormals; rx.bfloat = pp.bfloat; rx.dt = MXA_DT_F32;
   rx.codes = reinterpret_cast<int8_t*>(ws + L.xc);
   rx.sT = reinterpret_cast<int16_t*>(ws + L.xs);
   int rc = launch_rows_prep(rx, stream);
@@ -208,6 +208,7 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   pa.pe = reinterpret_cast<const int16_t*>(wb + W.pe);
   pa.ps = reinterpret_cast<const int16_t*>(wb + W.ps);
   pa.bias = xq.bias; pa.qkv_out = xq.qkv_out;
+  pa.autocast = xq.autocast_dtype;
   pa.B = pp.B; pa.N = pp.N; pa.H = pp.H; pa.D = pp.D; pa.nbk = nbk; pa.Cpad = Cpad; pa.bfloat = pp.bfloat;
   // shifted int32 block sums stay exact while nbk * 32 * 127^2 * 2^smax < 2^31
   pa.smax = -1;
@@ -232,6 +233,15 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
   if (!scores_only && p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
   if (p->pred_mode < MXA_PRED_EX_PRED || p->pred_mode > MXA_PRED_ELSA) return MXA_ERR_ARG;
+  if (p->dtype < MXA_DT_F32 || p->dtype > MXA_DT_BF16 || p->score_dtype < 0 || p->score_dtype > MXA_DT_BF16)
+    return MXA_ERR_ARG;
+  if (xq && (p->dtype != MXA_DT_F32 || (xq->autocast_dtype != 0 && xq->autocast_dtype != p->score_dtype)))
+    return MXA_ERR_ARG;  // the fused projection reads fp32 x; under autocast its scores follow autocast
+  // approximators whose operands are not exact in float16 / bfloat16 (EXION's e*(2^l1+2^l2),
+  // true_ex's per-element exponents, ELSA's fp32 projections): float32 only
+  if ((p->dtype != MXA_DT_F32 || p->score_dtype > MXA_DT_F32) && p->approx &&
+      (p->pred_mode == MXA_PRED_EXION || p->pred_mode == MXA_PRED_TRUE_EX || p->pred_mode == MXA_PRED_ELSA))
+    return MXA_ERR_UNSUPPORTED;
   if (p->bfloat != 0 && p->bfloat != 32 && (p->bfloat < 10 || p->bfloat > 31)) return MXA_ERR_ARG;
   if (p->T > 512 || p->D > 32 * kMaxNB) return MXA_ERR_UNSUPPORTED;
   mxa_attn_params pp = *p;
@@ -281,8 +291,9 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   RowsPrepArgs rq{};
   rq.x = pp.q; rq.s0 = pp.q_strides[0]; rq.s1 = pp.q_strides[1]; rq.s2 = pp.q_strides[2];
   rq.H = pp.H; rq.R = pp.N; rq.rows = BH * pp.N; rq.D = pp.D; rq.nb = L.nbd; rq.dpad = L.dpad;
-  rq.vec4 = aligned16(pp.q) && (pp.q_strides[0] % 4 == 0) && (pp.q_strides[1] % 4 == 0) && (pp.q_strides[2] % 4 == 0);
-  rq.op_kind = opq; rq.flush = pp.flush_subnormals; rq.bfloat = pp.bfloat;
+  const int64_t vpe = pp.dtype == MXA_DT_F32 ? 4 : 8;  // elements per 16 B
+  rq.vec4 = aligned16(pp.q) && (pp.q_strides[0] % vpe == 0) && (pp.q_strides[1] % vpe == 0) && (pp.q_strides[2] % vpe == 0);
+  rq.op_kind = opq; rq.flush = pp.flush_subnormals; rq.bfloat = pp.bfloat; rq.dt = xq ? MXA_DT_F32 : pp.dtype;
   rq.codes = reinterpret_cast<int8_t*>(ws + L.qc);
   rq.sT = reinterpret_cast<int16_t*>(ws + L.qsT);
   rq.op = need_op ? reinterpret_cast<int8_t*>(ws + L.qop) : nullptr;
@@ -294,7 +305,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   RowsPrepArgs rk = rq;
   rk.x = pp.k; rk.s0 = pp.k_strides[0]; rk.s1 = pp.k_strides[1]; rk.s2 = pp.k_strides[2];
   rk.R = pp.T; rk.rows = BH * pp.T;
-  rk.vec4 = aligned16(pp.k) && (pp.k_strides[0] % 4 == 0) && (pp.k_strides[1] % 4 == 0) && (pp.k_strides[2] % 4 == 0);
+  rk.vec4 = aligned16(pp.k) && (pp.k_strides[0] % vpe == 0) && (pp.k_strides[1] % vpe == 0) && (pp.k_strides[2] % vpe == 0);
   rk.op_kind = opk;
   rk.codes = reinterpret_cast<int8_t*>(ws + L.kc);
   rk.sT = reinterpret_cast<int16_t*>(ws + L.ksT);
@@ -305,7 +316,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   ColsPrepArgs cv{};
   cv.x = pp.v; cv.s0 = pp.v_strides[0]; cv.s1 = pp.v_strides[1]; cv.s2 = pp.v_strides[2];
   cv.H = pp.H; cv.mats = BH; cv.R = pp.T; cv.C = pp.D; cv.nb = L.ntb; cv.rpad = L.tpad;
-  cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat;
+  cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat; cv.dt = rq.dt;
   cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
   cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
   if (xq) {
@@ -354,6 +365,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.vt = reinterpret_cast<const int8_t*>(ws + L.vt);
   r2.vs = reinterpret_cast<const int16_t*>(ws + L.vs);
   r2.bfloat = pp.bfloat; r2.flush_p = pp.flush_subnormals; r2.scale = pp.scale;
+  r2.in_dt = pp.dtype;
+  r2.s_dt = pp.score_dtype > MXA_DT_F32 ? pp.score_dtype : pp.dtype;
   r2.bias = pp.bias;
   r2.bs0 = pp.bias_strides[0]; r2.bs1 = pp.bias_strides[1]; r2.bs2 = pp.bias_strides[2]; r2.bs3 = pp.bias_strides[3];
   r2.out = pp.out; r2.os0 = pp.out_strides[0]; r2.os1 = pp.out_strides[1]; r2.os2 = pp.out_strides[2];
@@ -438,11 +451,13 @@ extern "C" int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t 
          align_up(batch * nbk * Nc * 2);
 }
 
-extern "C" int mxa_matmul(const float* a, const float* b, float* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
+extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
                           int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a, int32_t elem_mbits_b,
-                          int32_t flush_subnormals, int32_t bfloat, void* workspace, int64_t workspace_bytes,
-                          hipStream_t stream) {
+                          int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype, int32_t b_dtype,
+                          int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
   if (!a || !b || !c || batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return MXA_ERR_ARG;
+  for (int dt : {a_dtype, b_dtype, c_dtype})
+    if (dt < MXA_DT_F32 || dt > MXA_DT_BF16) return MXA_ERR_ARG;
   if ((elem_mbits_a != 8 && elem_mbits_a != 4) || (elem_mbits_b != 8 && elem_mbits_b != 4))
     return MXA_ERR_UNSUPPORTED;
   if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
@@ -458,19 +473,20 @@ extern "C" int mxa_matmul(const float* a, const float* b, float* c, int64_t batc
   RowsPrepArgs ra{};
   ra.x = a; ra.s0 = a_batch_stride; ra.s1 = 0; ra.s2 = K; ra.H = 1; ra.R = M; ra.rows = batch * M;
   ra.D = K; ra.nb = nbk; ra.dpad = kpad;
-  ra.vec4 = aligned16(a) && (a_batch_stride % 4 == 0) && (K % 4 == 0);
+  const int64_t vpe = a_dtype == MXA_DT_F32 ? 4 : 8;
+  ra.vec4 = aligned16(a) && (a_batch_stride % vpe == 0) && (K % vpe == 0);
   ra.op_kind = elem_mbits_a == 8 ? MXA_OP_MXINT8 : MXA_OP_MXINT4;
-  ra.flush = flush_subnormals; ra.bfloat = bfloat;
+  ra.flush = flush_subnormals; ra.bfloat = bfloat; ra.dt = a_dtype;
   ra.codes = nullptr; ra.sT = nullptr; ra.op = ac; ra.sA = as;
   int rc = launch_rows_prep(ra, stream);
   if (rc) return rc;
   ColsPrepArgs cb{};
   cb.x = b; cb.s0 = b_batch_stride; cb.s1 = 0; cb.s2 = Nc; cb.H = 1; cb.mats = batch; cb.R = K; cb.C = Nc;
-  cb.nb = nbk; cb.rpad = kpad; cb.mbits = elem_mbits_b; cb.flush = flush_subnormals; cb.bfloat = bfloat;
+  cb.nb = nbk; cb.rpad = kpad; cb.mbits = elem_mbits_b; cb.flush = flush_subnormals; cb.bfloat = bfloat; cb.dt = b_dtype;
   cb.codes_t = bt; cb.scale = bsc;
   rc = launch_cols_prep(cb, stream);
   if (rc) return rc;
-  MatmulArgs ma{ac, as, bt, bsc, M, Nc, nbk, kpad, bfloat, c};
+  MatmulArgs ma{ac, as, bt, bsc, M, Nc, nbk, kpad, bfloat, c_dtype, c};
   dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 15) / 16), (unsigned)batch);
   hipLaunchKernelGGL(matmul_kernel, grid, dim3(256), 0, stream, ma);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;

@@ -7,6 +7,8 @@
 //   scale clamp       microxscaling/mx/mx_ops.py:276-300
 //   element rounding  microxscaling/mx/elemwise_ops.py:45-86, :92-180
 #pragma once
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -68,11 +70,100 @@ __device__ __forceinline__ int scale_exponent(uint32_t maxbits, int scale_emax, 
   return e < -scale_emax ? -scale_emax : e;
 }
 
+// ---- storage dtypes (include/mxa.h MXA_DT_*) ---------------------------------
+// The reference's mx ops follow their input's dtype (microxscaling/mx/mx_ops.py:85,
+// :283; elemwise_ops.py:146): on a float16 / bfloat16 tensor every step runs in that
+// dtype.  Element values convert exactly to float; what differs is (i) the shared
+// exponent, floor(log2(max)) with log2 rounded to the dtype, (ii) for float16 the
+// zero block: 2^-126 underflows to 0, log2(0) = -inf, the scale 2^-127 is 0 in
+// float16 and 0/0 makes the whole block NaN, and (iii) the rounding's |y| + 0.5 is
+// rounded to the dtype (round_code).  Probes in DESIGN.md §2.
+enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2 };
+
+__device__ __forceinline__ float bf16_bits_to_f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ float f16_bits_to_f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+// round-to-nearest-even to the dtype, returned as float (NaN stays NaN, overflow -> inf)
+__device__ __forceinline__ float round_dt(float x, int dt) {
+  if (dt == kF16) return __half2float(__float2half_rn(x));
+  if (dt == kBF16) {
+    const uint32_t u = __float_as_uint(x);
+    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return __uint_as_float(u | 0x00400000u);
+    return __uint_as_float(((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16) << 16);
+  }
+  return x;
+}
+__device__ __forceinline__ uint16_t f_to_dt_bits(float x, int dt) {
+  if (dt == kF16) return __half_as_ushort(__float2half_rn(x));
+  return (uint16_t)(__float_as_uint(round_dt(x, kBF16)) >> 16);
+}
+__device__ __forceinline__ float load_dt(const void* p, int64_t i, int dt) {
+  if (dt == kF16) return f16_bits_to_f(static_cast<const uint16_t*>(p)[i]);
+  if (dt == kBF16) return bf16_bits_to_f(static_cast<const uint16_t*>(p)[i]);
+  return static_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void store_dt(void* p, int64_t i, float v, int dt) {
+  if (dt == kF32) static_cast<float*>(p)[i] = v;
+  else static_cast<uint16_t*>(p)[i] = f_to_dt_bits(v, dt);
+}
+
+// floor(log2(m)) computed in the dtype, for m = |x| exactly representable in it, given
+// as float bits: log2 rounds up to the next integer for the top `gap` mantissa codes of
+// a binade, gap depending only on the octave of the exponent (float16: 0, 1, 2, 5;
+// bfloat16: 0, 1, 2, 5, 10, 21, 40), and for dtype subnormals above a per-leading-bit
+// threshold.  Restated by oracle/mx_oracle.py floor_log2_dtype and pinned against torch
+// on every value (tests/test_oracle_golden.py, tests/test_gpu_dtype.py).  Zero: float16
+// -> kExpZeroF16 (log2(0) = -inf), bfloat16 -> -126 (2^-126 is a bfloat16).
+constexpr int kExpZeroF16 = -100000;
+__device__ __forceinline__ int floor_log2_dt(uint32_t ub, int dt) {
+  if (dt == kF32) return floor_log2_abs_bits(ub);
+  if (ub >= 0x7F800000u) return kExpNaN;
+  if (ub == 0u) return dt == kF16 ? kExpZeroF16 : -126;
+  const int mb = dt == kF16 ? 10 : 7;
+  const int emin = dt == kF16 ? -14 : -126;
+  int e;        // floor(log2 m) exactly
+  uint32_t fm;  // float mantissa bits below the leading one (23 bits)
+  if (ub >= 0x00800000u) {
+    e = (int)(ub >> 23) - 127;
+    fm = ub & 0x7FFFFFu;
+  } else {  // float subnormal (bfloat16 subnormals only)
+    const int j = 31 - __clz((int)ub);
+    e = -149 + j;
+    fm = (ub << (23 - j)) & 0x7FFFFFu;
+  }
+  if (e >= emin) {  // normal in the dtype: mb mantissa bits
+    const uint32_t M = fm >> (23 - mb);
+    const uint32_t u = (uint32_t)(e >= 0 ? e : -e - 1);
+    const int o = u >= 2u ? 31 - __clz((int)u) : 0;  // octave of |e|
+    const uint32_t gap = dt == kF16 ? (uint32_t)(0x05020100u >> (8 * o)) & 0xFFu
+                                    : (uint32_t)(0x28150A05020100ull >> (8 * o)) & 0xFFu;
+    return e + (M + gap >= (1u << mb) ? 1 : 0);
+  }
+  // subnormal in the dtype: M = m / 2^(emin - mb), leading bit j
+  const int j = e - (emin - mb);
+  const uint32_t M = (1u << j) | (fm >> (23 - j));
+  uint32_t thr;  // smallest M of the sub-binade whose log2 rounds up (2^(j+1): none)
+  if (dt == kF16) thr = j == 9 ? 1022u : (j == 8 ? 511u : (j == 7 ? 255u : (2u << j)));
+  else thr = (uint32_t)(j == 0 ? 2 : (j == 1 ? 3 : (j == 2 ? 6 : (j == 3 ? 12 : (j == 4 ? 23 : (j == 5 ? 54 : 108))))));
+  return e + (M >= thr ? 1 : 0);
+}
+
+// scale_exponent for a block of a dtype tensor: the float16 zero block is NaN
+__device__ __forceinline__ int scale_exponent_dt(uint32_t maxbits, int scale_emax, int dt, int* e_raw) {
+  if (dt == kF32) return scale_exponent(maxbits, scale_emax, e_raw);
+  const int e = floor_log2_dt(maxbits, dt);
+  *e_raw = e == kExpZeroF16 ? -1000 : e;
+  if (e == kExpNaN || e == kExpZeroF16 || e > scale_emax) return kExpNaN;
+  return e < -scale_emax ? -scale_emax : e;
+}
+
 // Element rounding of x / 2^es * 2^(mbits-2) (elemwise_ops.py:45-65, :150-164);
 // returns the integer code as float, clamped to +-(2^(mbits-1)-1).
 // es is finite and in [-127, 127], so 2^-es is an exact float and x * 2^-es is
 // the correctly rounded x / 2^es.  Compiled with -ffp-contract=off.
-__device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd) {
+// On a float16 / bfloat16 tensor (dt) the reference adds the 0.5 in that dtype: |y| + 0.5
+// rounds to it (bfloat16 0.498046875 + 0.5 -> 1.0), so the sum is rounded to dt before the
+// floor (y itself is exact in dt: a power-of-two scaling of a dt value).
+__device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd, int dt = 0) {
   float y = x * pow2f(-es);
   y = y * (float)(1 << (mbits - 2));
   const float a = fabsf(y);
@@ -80,9 +171,9 @@ __device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd)
   if (rnd == kRoundFloor) {
     r = floorf(a);
   } else {
-    r = floorf(a + 0.5f);
+    r = floorf(round_dt(a + 0.5f, dt));
     if (rnd == kRoundEven) {
-      const float d = a - 0.5f;  // ((|A| - 0.5) % 2 == 0) -> step back to even
+      const float d = round_dt(a - 0.5f, dt);  // ((|A| - 0.5) % 2 == 0) -> step back to even
       if (floorf(d * 0.5f) * 2.0f == d) r -= 1.0f;
     }
   }
@@ -97,23 +188,25 @@ __device__ __forceinline__ float round_code(float x, int es, int mbits, int rnd)
 // the sign goes back on with a bit copy (-0 converts to 0 like +0).
 __device__ __forceinline__ float q8_scale(int es) { return pow2f(es >= -121 ? 6 - es : -es); }
 template <bool TINY>
-__device__ __forceinline__ int q8_code(float x, float s) {
+__device__ __forceinline__ int q8_code(float x, float s, int dt = 0) {
   float y = x * s;
   if (TINY) y = y * 64.0f;
-  const float r = fminf(floorf(fabsf(y) + 0.5f), 127.0f);
+  const float r = fminf(floorf(round_dt(fabsf(y) + 0.5f, dt)), 127.0f);
   return (int)__builtin_copysignf(r, y);
 }
 
 // bfloatX element quantization, exp_bits = 8, mbits = bfloat-7 (elemwise_ops.py:201-216
 // -> _quantize_elemwise_core :92-180 with saturate_normals=False).  bfloat in {0,32} = identity.
-__device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int allow_denorm) {
+// On a float16 / bfloat16 tensor (dt) the private exponent is floor(log2) computed in the
+// dtype (floor_log2_dt) and the result is a value of the dtype.
+__device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int allow_denorm, int dt = 0) {
   if (bfloat == 0 || bfloat == 32) return x;
   const uint32_t ub = __float_as_uint(x) & 0x7FFFFFFFu;
   if (ub >= 0x7F800000u) return x;  // +-Inf restored, NaN stays NaN
   const int bits = bfloat - 7;
   float xin = x;
   if (!allow_denorm && ub < 0x00800000u) xin = 0.0f * x;  // |A| < min_norm -> 0 (sign kept)
-  int pe = ub == 0u ? 0 : floor_log2_abs_bits(ub);  // log2(|A| + (A==0))
+  int pe = ub == 0u ? 0 : floor_log2_dt(ub, dt);  // log2(|A| + (A==0))
   pe = pe < -126 ? -126 : pe;
   float y = xin * pow2f(-pe);
   y = y * (float)(1 << (bits - 2));
@@ -122,9 +215,9 @@ __device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int 
   if (rnd == kRoundFloor) {
     r = floorf(a);
   } else {
-    r = floorf(a + 0.5f);
+    r = floorf(round_dt(a + 0.5f, dt));
     if (rnd == kRoundEven) {
-      const float d = a - 0.5f;
+      const float d = round_dt(a - 0.5f, dt);
       if (floorf(d * 0.5f) * 2.0f == d) r -= 1.0f;
     }
   }
@@ -132,7 +225,7 @@ __device__ __forceinline__ float round_bfloat(float x, int bfloat, int rnd, int 
   o = o * pow2f(pe > 127 ? 127 : pe);
   const float max_norm = 1.7014118346046923e38f * ((float)((1 << (bits - 1)) - 1) / (float)(1 << (bits - 2)));
   if (fabsf(o) > max_norm) o = o < 0.0f ? -INFINITY : INFINITY;
-  return o;
+  return round_dt(o, dt);
 }
 
 // ---- wave64 helpers -------------------------------------------------------

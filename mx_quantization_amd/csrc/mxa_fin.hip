@@ -74,18 +74,23 @@ static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg
   *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
   return MXA_OK;
 }
-template <int NB, int KS, bool PAIR>
-static int launch_finish_ks(const Rows2Args& ra0, int BH, hipStream_t stream) {
+template <int NB, int KS, bool PAIR, bool XDT>
+static int launch_finish_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
   int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
   const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR).total;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR, XDT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR, XDT>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NB, int KS, bool PAIR>
+static int launch_finish_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish_xdt<NB, KS, PAIR, true>(ra, BH, stream);
+  return launch_finish_xdt<NB, KS, PAIR, false>(ra, BH, stream);
 }
 template <int NB>
 static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {

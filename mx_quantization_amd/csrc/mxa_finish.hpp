@@ -67,8 +67,11 @@ __device__ __forceinline__ float scale_f(int e) {
 // PAIR = true: the tile's 32 rows in ONE pass, two lanes per query row (k <= 2 KS <= 32,
 //   DeiT's k = 20): every lane busy, one round of softmax / MX(P) synchronisation per
 //   tile instead of eight.
-template <int NB, int KS, bool PAIR>
+// XDT: float16 / bfloat16 inputs or scores (include/mxa.h dtype / score_dtype): the
+// dtype roundings at run time; XDT = false compiles them away (the float32 path).
+template <int NB, int KS, bool PAIR, bool XDT>
 __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
+  const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
   const int bh = blockIdx.x;
@@ -176,12 +179,15 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
       const int r = r0 + pr;
       const bool valid = r < r_end;
       const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
-      const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
+      const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
       auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
         bool nan = false;
         const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
-        float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
-        if (brow) t = t + brow[(int64_t)j * a.bs3];
+        // (true scores in the score dtype: the matmul's output, then * scale, + bias)
+        float t = round_bfloat(round_dt(nan ? __uint_as_float(0x7FC00000u) : (float)acc, sdt), a.bfloat, kRoundNearest,
+                              1, sdt);
+        t = round_dt(t * a.scale, sdt);
+        if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);
         return t;
       };
       if (a.true_out && valid)  // debug output: every key's true score
@@ -205,14 +211,14 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
 #pragma unroll
       for (int t = 0; t < KS; ++t) {
         if (cur.ix[t] >= 0) {
-          v[t] = round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1);
+          v[t] = round_dt(round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1, sdt), sdt);
           atomicMax(&bm[cur.ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
         }
       }
       wave_lds_sync();
       for (int bk = ph; bk < ntb; bk += 2) {  // block bk: scale exponent (+1024; 0 = NaN block), flush flag
         int e_raw;
-        const int es = scale_exponent(bm[bk], 127, &e_raw);
+        const int es = scale_exponent_dt(bm[bk], 127, sdt, &e_raw);
         const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
         sP[bk * kFinTile + pr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
         bm[bk] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
           if (e & 0xFFFFu) {
             const int es = (int)(e & 0xFFFFu) - 1024;
             const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
-            code = (int)round_code(x, es, 8, kRoundNearest);
+            code = (int)round_code(x, es, 8, kRoundNearest, sdt);
           }
           ptile[pr * vst + cur.ix[t]] = (int8_t)code;
         }
@@ -244,12 +250,15 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
         const int r = r0 + tr;
         const bool valid = r < r_end;
         const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
-        const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : nullptr;
+        const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
         auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
           bool nan = false;
           const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
-          float t = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
-          if (brow) t = t + brow[(int64_t)j * a.bs3];
+          // (true scores in the score dtype: the matmul's output, then * scale, + bias)
+          float t = round_bfloat(round_dt(nan ? __uint_as_float(0x7FC00000u) : (float)acc, sdt), a.bfloat, kRoundNearest,
+                                1, sdt);
+          t = round_dt(t * a.scale, sdt);
+          if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);
           return t;
         };
         if (a.true_out && valid)  // debug output: every key's true score
@@ -280,14 +289,14 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   #pragma unroll
         for (int t = 0; t < KS; ++t) {
           if (ix[t] >= 0) {
-            v[t] = round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1);
+            v[t] = round_dt(round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1, sdt), sdt);
             atomicMax(&bm[ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
           }
         }
         wave_lds_sync();
         if (gl < ntb) {  // block gl: scale exponent (+1024; 0 = NaN block) and flush flag
           int e_raw;
-          const int es = scale_exponent(bm[gl], 127, &e_raw);
+          const int es = scale_exponent_dt(bm[gl], 127, sdt, &e_raw);
           const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
           sP[gl * kFinTile + tr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
           bm[gl] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
             if (e & 0xFFFFu) {
               const int es = (int)(e & 0xFFFFu) - 1024;
               const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
-              code = (int)round_code(x, es, 8, kRoundNearest);
+              code = (int)round_code(x, es, 8, kRoundNearest, sdt);
             }
             ptile[tr * vst + ix[t]] = (int8_t)code;
           }
@@ -344,7 +353,8 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
         for (int i = 0; i < 16; ++i) {
           const int r = r0 + 8 * (i >> 2) + m0 + (i & 3);
           if (r < r_end)
-            a.out[b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + dt + ln] = round_bfloat(acc[i], a.bfloat, kRoundNearest, 1);
+            store_dt(a.out, b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + dt + ln,
+                     round_bfloat(round_dt(acc[i], sdt), a.bfloat, kRoundNearest, 1, sdt), sdt);
         }
       }
     }

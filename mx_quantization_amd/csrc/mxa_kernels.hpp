@@ -7,38 +7,39 @@
 namespace mxa {
 
 struct QuantArgs {
-  const float* x;
-  float* y;
+  const void* x;  // dtype dt
+  void* y;        // dtype dt
   int8_t* codes;
   int16_t* exps;
   int64_t outer, L, inner, bs, nb;
-  int mbits, scale_emax, rnd, flush, bfloat;
+  int mbits, scale_emax, rnd, flush, bfloat, dt;
 };
 
 struct SexpArgs {
-  const float* x;
-  float* out;
+  const void* x;  // dtype dt
+  void* out;      // dtype dt
   int64_t outer, L, inner, bs, nb;
-  int method, ebits;
+  int method, ebits, dt;
 };
 
 struct ApproxArgs {
-  const float* x;
-  float* out;
+  const void* x;  // dtype dt
+  void* out;      // dtype dt
   int64_t rows;
   int d;
   int64_t ld_x, ld_out;
-  int op_kind, flush, bfloat;
+  int op_kind, flush, bfloat, dt;
 };
 
 // rows of D elements at x + b*s0 + h*s1 + r*s2 (r < R, h < H), quantized along D
 struct RowsPrepArgs {
-  const float* x;
+  const void* x;  // dtype dt
   int64_t s0, s1, s2;
   int64_t H, R, rows;  // rows = B*H*R
   int D, nb, dpad;
   int vec4;  // 16-B aligned rows -> float4 loads
   int op_kind, flush, bfloat;
+  int dt;         // storage dtype of x (MXA_DT_*): loads and the shared-exponent rule
   int8_t* codes;  // [rows][dpad] MXINT8 codes (nullable)
   int16_t* sT;    // [rows][nb] exponent of a code unit: es - 6 (nullable)
   int8_t* op;     // [rows][dpad] approximator operand (nullable)
@@ -62,11 +63,12 @@ struct ElsaPrepArgs {
 
 // matrices (R x C) at x + b*s0 + h*s1 + r*s2 + c quantized along R in 32-blocks
 struct ColsPrepArgs {
-  const float* x;
+  const void* x;  // dtype dt
   int64_t s0, s1, s2;
   int64_t H, mats;  // mats = B*H
   int R, C, nb, rpad;
   int mbits, flush, bfloat;
+  int dt;  // storage dtype of x
   int8_t* codes_t;  // [mats][C][rpad] transposed codes
   int16_t* scale;   // [mats][nb][C] exponent of a code unit: es - (mbits-2)
 };

@@ -42,13 +42,13 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
   uint32_t mb = 0;
 #pragma unroll
   for (int j = 0; j < EPL; ++j) {
-    xv[j] = round_bfloat(xv[j], a.bfloat, kRoundNearest, 1);
+    xv[j] = round_bfloat(xv[j], a.bfloat, kRoundNearest, 1, a.dt);
     const uint32_t ub = __float_as_uint(xv[j]) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;
   }
   mb = blk_reduce<LPB>(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   int e_raw;
-  const int es = scale_exponent(mb, 127, &e_raw);
+  const int es = scale_exponent_dt(mb, 127, a.dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   if (a.flush && !(e_raw != kExpNaN && e_raw > -127)) {
 #pragma unroll
@@ -58,17 +58,18 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
   int maxc = 0;
 #pragma unroll
   for (int j = 0; j < EPL; ++j) {
-    code[j] = nanblk ? 0 : (int)round_code(xv[j], es, 8, kRoundNearest);
+    code[j] = nanblk ? 0 : (int)round_code(xv[j], es, 8, kRoundNearest, a.dt);
     const int ac = code[j] < 0 ? -code[j] : code[j];
     maxc = ac > maxc ? ac : maxc;
   }
   maxc = (int)blk_reduce<LPB>((uint32_t)maxc, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
-  // floor(log2(max |MX|)), unclamped; MX max = maxc * 2^(es-6) exactly.
+  // floor(log2(max |MX|)), unclamped, in the dtype; MX max = maxc * 2^(es-6) (a value
+  // of the dtype: exact in float32 / bfloat16, and in float16 for es >= -18)
   int eA;
   if (nanblk) eA = kExpNaN;
   else if (maxc == 0) eA = -126;
-  else eA = floor_log2_pos((float)maxc * pow2f(es - 6));
+  else eA = floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), a.dt)), a.dt);
   int op[EPL];
   int sA;
   switch (a.op_kind) {
@@ -79,7 +80,7 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       break;
     case MXA_OP_MXINT4:
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest);
+      for (int j = 0; j < EPL; ++j) op[j] = nanblk ? 0 : (int)round_code(xv[j], es, 4, kRoundNearest, a.dt);
       sA = nanblk ? kExpNaN : es - 2;
       break;
     case MXA_OP_EXION: {
@@ -162,13 +163,13 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
   for (int j = 0; j < EPL; ++j) mb = max(mb, __float_as_uint(xv[j]) & 0x7FFFFFFFu);
   mb = blk_reduce<LPB>(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   int e_raw;
-  const int es = scale_exponent(mb, 127, &e_raw);
+  const int es = scale_exponent_dt(mb, 127, a.dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   int code[EPL];
   auto quant = [&](auto tiny) {
     const float s = q8_scale(es);
 #pragma unroll
-    for (int j = 0; j < EPL; ++j) code[j] = q8_code<decltype(tiny)::value>(xv[j], s);
+    for (int j = 0; j < EPL; ++j) code[j] = q8_code<decltype(tiny)::value>(xv[j], s, a.dt);
   };
   if (nanblk) {
 #pragma unroll
@@ -205,7 +206,9 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
     if (sub == 0) {
       // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
       // floor(log2(maxc * 2^(es-6))) = floor(log2 maxc) + es - 6 exactly (maxc <= 127)
-      const int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : 31 - __clz(maxc) + es - 6);
+      int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : 31 - __clz(maxc) + es - 6);
+      if (a.dt != kF32 && !nanblk && maxc != 0)  // log2 rounded to the dtype
+        eA = floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), a.dt)), a.dt);
       if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
       if (a.sA) a.sA[row * a.nb + blk] = exp_to16(a.op_kind == MXA_OP_SIGN ? eA : (nanblk ? kExpNaN : es - 6));
       if (a.signs) a.signs[row * a.nb + blk] = sw;
@@ -224,7 +227,7 @@ __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t 
                                                  uint32_t mx) {
   const int r0 = blk * 32;
   int e_raw;
-  const int es = scale_exponent(mx, 127, &e_raw);
+  const int es = scale_exponent_dt(mx, 127, a.dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
   uint32_t w[8];
@@ -235,7 +238,7 @@ __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t 
       for (int q = 0; q < 8; ++q) {
         int cd[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cd[j] = q8_code<decltype(tiny)::value>(xv[q * 4 + j], s);
+        for (int j = 0; j < 4; ++j) cd[j] = q8_code<decltype(tiny)::value>(xv[q * 4 + j], s, a.dt);
         w[q] = (uint32_t)(cd[0] & 0xFF) | (uint32_t)(cd[1] & 0xFF) << 8 | (uint32_t)(cd[2] & 0xFF) << 16 |
                (uint32_t)cd[3] << 24;
       }
@@ -250,7 +253,7 @@ __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t 
       for (int j = 0; j < 4; ++j) {
         float v = xv[q * 4 + j];
         if (flush) v = v * 0.0f;
-        const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest);
+        const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest, a.dt);
         acc |= (uint32_t)(cd & 0xFF) << (8 * j);
       }
       w[q] = acc;

@@ -223,6 +223,7 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
         else o = (float)acc[i];
         if (cnan || rn[m]) o = __uint_as_float(0x7FC00000u);
         o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+        o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
         if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
         if (colv) {
           ot[m * L.ost + s * D + dcol] = o;

@@ -49,6 +49,7 @@ struct ProjArgs {
   int B, N, H, D, nbk, Cpad, bfloat;
   int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
   int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
+  int autocast;  // 0, or the dtype torch.autocast rounds the product to before the fp32 bias add
   RowsPrepArgs rq, rk;  // q / k row outputs (rows_prep layout)
   ColsPrepArgs cv;      // V outputs (cols_prep layout)
 };

@@ -29,28 +29,29 @@ __global__ __launch_bounds__(256) void quantize_mx_kernel(QuantArgs a) {
   const int64_t o = ob / a.nb;
   const int64_t l0 = blk * a.bs;
   const int64_t l1 = (l0 + a.bs < a.L) ? l0 + a.bs : a.L;
-  const float* xp = a.x + (o * a.L) * a.inner + i;
+  const int64_t xp = (o * a.L) * a.inner + i;
   uint32_t mb = 0;
   for (int64_t l = l0; l < l1; ++l) {
-    const uint32_t ub = __float_as_uint(round_bfloat(xp[l * a.inner], a.bfloat, kRoundNearest, 1)) & 0x7FFFFFFFu;
+    const float xv = round_bfloat(load_dt(a.x, xp + l * a.inner, a.dt), a.bfloat, kRoundNearest, 1, a.dt);
+    const uint32_t ub = __float_as_uint(xv) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;
   }
   int e_raw;
-  const int es = scale_exponent(mb, a.scale_emax, &e_raw);
+  const int es = scale_exponent_dt(mb, a.scale_emax, a.dt, &e_raw);
   const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
   const int shift = a.mbits - 2;
   for (int64_t l = l0; l < l1; ++l) {
-    float xv = round_bfloat(xp[l * a.inner], a.bfloat, kRoundNearest, 1);
+    float xv = round_bfloat(load_dt(a.x, xp + l * a.inner, a.dt), a.bfloat, kRoundNearest, 1, a.dt);
     if (flush) xv = xv * 0.0f;
     float yv, cv = 0.0f;
     if (es == kExpNaN) {
       yv = __uint_as_float(0x7FC00000u);
     } else {
-      cv = round_code(xv, es, a.mbits, a.rnd);
+      cv = round_code(xv, es, a.mbits, a.rnd, a.dt);
       yv = (cv * pow2f(-shift)) * pow2f(es);
     }
     const int64_t off = (o * a.L + l) * a.inner + i;
-    a.y[off] = yv;
+    store_dt(a.y, off, yv, a.dt);  // (code * 2^(es-shift) rounded once to the dtype)
     if (a.codes) a.codes[off] = (int8_t)cv;
   }
   if (a.exps) a.exps[(o * a.nb + blk) * a.inner + i] = exp_to16(es);
@@ -59,10 +60,12 @@ __global__ __launch_bounds__(256) void quantize_mx_kernel(QuantArgs a) {
 // ---------------------------------------------------------------------------
 // shared exponents (method "max" per block, or "none" per element)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float sexp_value(uint32_t ub, int ebits) {
-  int e = floor_log2_abs_bits(ub & 0x7FFFFFFFu);
+__device__ __forceinline__ float sexp_value(uint32_t ub, int ebits, int dt) {
+  int e = floor_log2_dt(ub & 0x7FFFFFFFu, dt);
   float v;
-  if (e == kExpNaN) {
+  if (e == kExpZeroF16) {
+    v = -INFINITY;  // float16: 2^-126 underflows, log2(0) = -inf
+  } else if (e == kExpNaN) {
     // log2(inf) = inf -> floor = inf; NaN stays NaN
     v = ((ub & 0x7FFFFFFFu) == 0x7F800000u) ? INFINITY : __uint_as_float(0x7FC00000u);
   } else {
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(256) void shared_exp_kernel(SexpArgs a) {
   if (a.method == 1) {  // none: elementwise
     const int64_t n = a.outer * a.L * a.inner;
     if (t >= n) return;
-    a.out[t] = sexp_value(__float_as_uint(a.x[t]) & 0x7FFFFFFFu, a.ebits);
+    store_dt(a.out, t, sexp_value(__float_as_uint(load_dt(a.x, t, a.dt)) & 0x7FFFFFFFu, a.ebits, a.dt), a.dt);
     return;
   }
   const int64_t nblocks = a.outer * a.nb * a.inner;
@@ -94,28 +97,65 @@ __global__ __launch_bounds__(256) void shared_exp_kernel(SexpArgs a) {
   const int64_t l1 = (l0 + a.bs < a.L) ? l0 + a.bs : a.L;
   uint32_t mb = 0;
   for (int64_t l = l0; l < l1; ++l) {
-    const uint32_t ub = __float_as_uint(a.x[(o * a.L + l) * a.inner + i]) & 0x7FFFFFFFu;
+    const uint32_t ub = __float_as_uint(load_dt(a.x, (o * a.L + l) * a.inner + i, a.dt)) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;  // NaN bits compare above Inf: max propagates NaN like torch.max
   }
-  a.out[t] = sexp_value(mb, a.ebits);
+  store_dt(a.out, t, sexp_value(mb, a.ebits, a.dt), a.dt);
 }
 
 // ---------------------------------------------------------------------------
 // elementwise bfloat quantization (vectorized, grid-stride)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bfloat_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
-                                                     int bfloat, int rnd, int allow_denorm) {
+__global__ __launch_bounds__(256) void bfloat_kernel(const void* __restrict__ x, void* __restrict__ y, int64_t n,
+                                                     int bfloat, int rnd, int allow_denorm, int dt) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride)
-    y[t] = round_bfloat(x[t], bfloat, rnd, allow_denorm);
+    store_dt(y, t, round_bfloat(load_dt(x, t, dt), bfloat, rnd, allow_denorm, dt), dt);
 }
 
 // ---------------------------------------------------------------------------
 // attention operand builder for rows quantized along the last axis (Q, K):
 // 8 lanes per 32-element block, 4 floats (16 B) per lane (body: mxa_prep.hpp)
 // ---------------------------------------------------------------------------
+// 16 consecutive elements of a row (from element c0) of storage dtype DT as floats
+template <int DT>
+__device__ __forceinline__ void load_row16(const void* xr, int c0, int D, bool vec, bool valid, float xv[16]) {
+  if constexpr (DT == kF32) {
+    const float* x = static_cast<const float*>(xr);
+    if (valid && vec && c0 + 16 <= D) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(x + c0 + 4 * q);
+        xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = (valid && c0 + j < D) ? x[c0 + j] : 0.0f;
+    }
+  } else {
+    const uint16_t* x = static_cast<const uint16_t*>(xr);
+    auto cvt = [](uint16_t h) { return DT == kF16 ? f16_bits_to_f(h) : bf16_bits_to_f(h); };
+    if (valid && vec && c0 + 16 <= D) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(x + c0 + 8 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          xv[8 * q + 2 * t] = cvt((uint16_t)(w[t] & 0xFFFFu));
+          xv[8 * q + 2 * t + 1] = cvt((uint16_t)(w[t] >> 16));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = (valid && c0 + j < D) ? cvt(x[c0 + j]) : 0.0f;
+    }
+  }
+}
+
+template <int DT>
 __device__ __forceinline__ void rows_prep_body(const RowsPrepArgs& a, uint32_t bid) {
-  // two lanes per 32-element block, 16 floats (4 x 16 B) per lane; 32-bit index math
+  // two lanes per 32-element block, 16 elements per lane; 32-bit index math
   // (the launcher checks rows * nb < 2^31): a 64-bit division is a ~50-instruction
   // software sequence per thread, 32-bit ~10
   const uint32_t gt = bid * 256u + threadIdx.x;
@@ -132,28 +172,22 @@ __device__ __forceinline__ void rows_prep_body(const RowsPrepArgs& a, uint32_t b
   const uint32_t b32 = bh32 / H;
   const int64_t h = bh32 - b32 * H;
   const int64_t b = b32;
-  const float* xr = a.x + b * a.s0 + h * a.s1 + r * a.s2;
+  constexpr int esz = DT == kF32 ? 4 : 2;
+  const void* xr = static_cast<const char*>(a.x) + (b * a.s0 + h * a.s1 + r * a.s2) * esz;
   const int c0 = blk * 32 + sub * 16;
   float xv[16];
-  if (valid && a.vec4 && c0 + 16 <= a.D) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + c0 + 4 * q);
-      xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) xv[j] = (valid && c0 + j < a.D) ? xr[c0 + j] : 0.0f;
-  }
+  load_row16<DT>(xr, c0, a.D, a.vec4, valid, xv);
   if (rows_prep_plain(a)) rows_prep_block_plain<16>(a, row, blk, sub, c0, xv, valid);
   else rows_prep_block<16>(a, row, blk, sub, c0, xv, valid);
 }
-__global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) { rows_prep_body(a, blockIdx.x); }
+template <int DT>
+__global__ __launch_bounds__(256) void rows_prep_kernel(RowsPrepArgs a) { rows_prep_body<DT>(a, blockIdx.x); }
 
 // ---------------------------------------------------------------------------
 // operand builder for matrices quantized along the row axis (V, and in2 of
 // mx.matmul): one thread per (matrix, block, column), coalesced along columns
 // ---------------------------------------------------------------------------
+template <int DT>
 __device__ __forceinline__ void cols_prep_body(const ColsPrepArgs& a, uint32_t bid) {
   // 32-bit index math (the launcher checks the thread count fits)
   const uint32_t t = bid * 256u + threadIdx.x;
@@ -168,32 +202,34 @@ __device__ __forceinline__ void cols_prep_body(const ColsPrepArgs& a, uint32_t b
   const int64_t m = m32;
   const int64_t h = m32 - b32 * H;
   const int64_t b = b32;
-  const float* xc = a.x + b * a.s0 + h * a.s1 + c;
+  const int64_t base = b * a.s0 + h * a.s1 + c;
   const int r0 = blk * 32;
   float xv[32];
   uint32_t mx = 0;
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     const int rr = r0 + j;
-    float v = rr < a.R ? xc[(int64_t)rr * a.s2] : 0.0f;
-    v = round_bfloat(v, a.bfloat, kRoundNearest, 1);
+    float v = rr < a.R ? load_dt(a.x, base + (int64_t)rr * a.s2, DT) : 0.0f;
+    v = round_bfloat(v, a.bfloat, kRoundNearest, 1, DT);
     xv[j] = v;
     const uint32_t ub = __float_as_uint(v) & 0x7FFFFFFFu;
     mx = ub > mx ? ub : mx;
   }
   cols_prep_column(a, m, blk, c, xv, mx);
 }
-__global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) { cols_prep_body(a, blockIdx.x); }
+template <int DT>
+__global__ __launch_bounds__(256) void cols_prep_kernel(ColsPrepArgs a) { cols_prep_body<DT>(a, blockIdx.x); }
 
 // The attention path's three operand builders in ONE launch (no launch gaps / tails
 // between them): blocks [0, nq) quantize Q rows, [nq, nq + nk) K rows, the rest V
 // columns.  The role is uniform per workgroup.
+template <int DT>
 __global__ __launch_bounds__(256) void attn_prep_kernel(RowsPrepArgs q, RowsPrepArgs k, ColsPrepArgs v, uint32_t nq,
                                                         uint32_t nk) {
   const uint32_t b = blockIdx.x;
-  if (b < nq) rows_prep_body(q, b);
-  else if (b < nq + nk) rows_prep_body(k, b - nq);
-  else cols_prep_body(v, b - nq - nk);
+  if (b < nq) rows_prep_body<DT>(q, b);
+  else if (b < nq + nk) rows_prep_body<DT>(k, b - nq);
+  else cols_prep_body<DT>(v, b - nq - nk);
 }
 
 // ---------------------------------------------------------------------------
@@ -251,38 +287,41 @@ __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
   if (t >= a.rows * nb) return;
   const int64_t row = t / nb;
   const int blk = (int)(t % nb);
-  const float* xr = a.x + row * a.ld_x;
-  float* yr = a.out + row * a.ld_out;
+  const int dt = a.dt;
+  const int64_t xr = row * a.ld_x, yr = row * a.ld_out;
   const int c0 = blk * 32, c1 = (c0 + 32 < a.d) ? c0 + 32 : a.d;
+  auto in = [&](int c) { return round_bfloat(load_dt(a.x, xr + c, dt), a.bfloat, kRoundNearest, 1, dt); };
   uint32_t mb = 0;
   for (int c = c0; c < c1; ++c) {
-    const uint32_t ub = __float_as_uint(round_bfloat(xr[c], a.bfloat, kRoundNearest, 1)) & 0x7FFFFFFFu;
+    const uint32_t ub = __float_as_uint(in(c)) & 0x7FFFFFFFu;
     mb = ub > mb ? ub : mb;
   }
   int e_raw;
-  const int es = scale_exponent(mb, 127, &e_raw);
+  const int es = scale_exponent_dt(mb, 127, dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
   const float qnan = __uint_as_float(0x7FC00000u);
   int maxc = 0;
   for (int c = c0; c < c1; ++c) {
-    float xv = round_bfloat(xr[c], a.bfloat, kRoundNearest, 1);
+    float xv = in(c);
     if (flush) xv = xv * 0.0f;
-    const int cd = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+    const int cd = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest, dt);
     maxc = (cd < 0 ? -cd : cd) > maxc ? (cd < 0 ? -cd : cd) : maxc;
   }
-  const int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : floor_log2_pos((float)maxc * pow2f(es - 6)));
+  // exponent of the MX block (in the dtype: the MX max is a value of the dtype)
+  const int eA = nanblk ? kExpNaN
+                        : (maxc == 0 ? -126 : floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), dt)), dt));
   for (int c = c0; c < c1; ++c) {
-    float xv = round_bfloat(xr[c], a.bfloat, kRoundNearest, 1);
+    float xv = in(c);
     if (flush) xv = xv * 0.0f;
     float out;
     if (nanblk) {
       out = a.op_kind == MXA_OP_TRUE_EX ? 1.0f : qnan;  // true_ex: NaN -> exponent 0 -> +1 (examples :98-110)
     } else if (a.op_kind == MXA_OP_MXINT4) {
-      out = (round_code(xv, es, 4, kRoundNearest) * 0.25f) * pow2f(es);
+      out = (round_code(xv, es, 4, kRoundNearest, dt) * 0.25f) * pow2f(es);
     } else {
-      const int cd = (int)round_code(xv, es, 8, kRoundNearest);
-      const float mxv = ((float)cd * pow2f(-6)) * pow2f(es);  // MX int8 value
+      const int cd = (int)round_code(xv, es, 8, kRoundNearest, dt);
+      const float mxv = round_dt(((float)cd * pow2f(-6)) * pow2f(es), dt);  // MX int8 value
       switch (a.op_kind) {
         case MXA_OP_SIGN:  // (mx < 0 ? -1 : +1) * 2^eA
           out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(eA);
@@ -295,7 +334,7 @@ __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
         }
         case MXA_OP_TRUE_EX: {  // (mx < 0 ? -1 : +1) * 2^(floor(log2|mx|)), zeros -> 2^0
           const float am = fabsf(mxv);
-          const int te = am > 0.0f ? floor_log2_pos(am) : 0;
+          const int te = am > 0.0f ? floor_log2_dt(__float_as_uint(am), dt) : 0;
           out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(te);
           break;
         }
@@ -303,7 +342,7 @@ __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
           out = mxv;
       }
     }
-    yr[c] = out;
+    store_dt(a.out, yr + c, round_dt(out, dt), dt);
   }
 }
 
@@ -314,11 +353,13 @@ using namespace mxa;
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-extern "C" int mxa_quantize_mx(const float* x, float* y, int8_t* codes, int16_t* exps, int64_t outer,
+static bool dtype_ok(int dt) { return dt == kF32 || dt == kF16 || dt == kBF16; }
+
+extern "C" int mxa_quantize_mx(const void* x, void* y, int8_t* codes, int16_t* exps, int64_t outer,
                                int64_t axis_len, int64_t inner, int32_t block_size, int32_t elem_mbits,
                                int32_t scale_bits, int32_t round_mode, int32_t flush_subnormals, int32_t bfloat,
-                               hipStream_t stream) {
-  if (!x || !y || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0) return MXA_ERR_ARG;
+                               int32_t dtype, hipStream_t stream) {
+  if (!x || !y || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0 || !dtype_ok(dtype)) return MXA_ERR_ARG;
   if (elem_mbits != 8 && elem_mbits != 4 && elem_mbits != 2) return MXA_ERR_UNSUPPORTED;
   if (scale_bits < 2 || scale_bits > 8 || round_mode < 0 || round_mode > 2) return MXA_ERR_ARG;
   if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
@@ -329,48 +370,50 @@ extern "C" int mxa_quantize_mx(const float* x, float* y, int8_t* codes, int16_t*
   a.bs = block_size == 0 ? axis_len : block_size;
   a.nb = (axis_len + a.bs - 1) / a.bs;
   a.mbits = elem_mbits; a.scale_emax = (1 << (scale_bits - 1)) - 1; a.rnd = round_mode;
-  a.flush = flush_subnormals; a.bfloat = bfloat;
+  a.flush = flush_subnormals; a.bfloat = bfloat; a.dt = dtype;
   const int64_t nblocks = outer * a.nb * inner;
   hipLaunchKernelGGL(quantize_mx_kernel, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
-extern "C" int mxa_shared_exponents(const float* x, float* out, int64_t outer, int64_t axis_len, int64_t inner,
-                                    int32_t block_size, int32_t method, int32_t ebits, hipStream_t stream) {
-  if (!x || !out || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0) return MXA_ERR_ARG;
+extern "C" int mxa_shared_exponents(const void* x, void* out, int64_t outer, int64_t axis_len, int64_t inner,
+                                    int32_t block_size, int32_t method, int32_t ebits, int32_t dtype,
+                                    hipStream_t stream) {
+  if (!x || !out || outer < 0 || axis_len < 0 || inner < 0 || block_size < 0 || !dtype_ok(dtype)) return MXA_ERR_ARG;
   if (method != 0 && method != 1) return MXA_ERR_ARG;
   if (outer == 0 || axis_len == 0 || inner == 0) return MXA_OK;
   SexpArgs a{};
   a.x = x; a.out = out; a.outer = outer; a.L = axis_len; a.inner = inner;
   a.bs = block_size == 0 ? axis_len : block_size;
   a.nb = (axis_len + a.bs - 1) / a.bs;
-  a.method = method; a.ebits = ebits;
+  a.method = method; a.ebits = ebits; a.dt = dtype;
   const int64_t n = method == 1 ? outer * axis_len * inner : outer * a.nb * inner;
   hipLaunchKernelGGL(shared_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
-extern "C" int mxa_quantize_bfloat(const float* x, float* y, int64_t n, int32_t bfloat, int32_t round_mode,
-                                   int32_t allow_denorm, hipStream_t stream) {
-  if (!x || !y || n < 0) return MXA_ERR_ARG;
+extern "C" int mxa_quantize_bfloat(const void* x, void* y, int64_t n, int32_t bfloat, int32_t round_mode,
+                                   int32_t allow_denorm, int32_t dtype, hipStream_t stream) {
+  if (!x || !y || n < 0 || !dtype_ok(dtype)) return MXA_ERR_ARG;
   if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
   if (round_mode < 0 || round_mode > 2) return MXA_ERR_ARG;
   if (n == 0) return MXA_OK;
   int64_t blocks = (n + 255) / 256;
   if (blocks > 256 * 16) blocks = 256 * 16;
   hipLaunchKernelGGL(bfloat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, n, bfloat, round_mode,
-                     allow_denorm);
+                     allow_denorm, dtype);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
-extern "C" int mxa_approx_values(const float* x, float* out, int64_t rows, int32_t d, int64_t ld_x, int64_t ld_out,
-                                 int32_t op_kind, int32_t flush_subnormals, int32_t bfloat, hipStream_t stream) {
-  if (!x || !out || rows < 0 || d <= 0 || ld_x < d || ld_out < d) return MXA_ERR_ARG;
+extern "C" int mxa_approx_values(const void* x, void* out, int64_t rows, int32_t d, int64_t ld_x, int64_t ld_out,
+                                 int32_t op_kind, int32_t flush_subnormals, int32_t bfloat, int32_t dtype,
+                                 hipStream_t stream) {
+  if (!x || !out || rows < 0 || d <= 0 || ld_x < d || ld_out < d || !dtype_ok(dtype)) return MXA_ERR_ARG;
   if (op_kind < MXA_OP_SIGN || op_kind > MXA_OP_TRUE_EX) return MXA_ERR_ARG;
   if (rows == 0) return MXA_OK;
   ApproxArgs a{};
   a.x = x; a.out = out; a.rows = rows; a.d = d; a.ld_x = ld_x; a.ld_out = ld_out;
-  a.op_kind = op_kind; a.flush = flush_subnormals; a.bfloat = bfloat;
+  a.op_kind = op_kind; a.flush = flush_subnormals; a.bfloat = bfloat; a.dt = dtype;
   const int64_t n = rows * ((d + 31) / 32);
   hipLaunchKernelGGL(approx_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
@@ -381,7 +424,10 @@ int launch_rows_prep(const RowsPrepArgs& a, hipStream_t stream) {
   const int64_t threads = a.rows * a.nb * 2;
   if (threads == 0) return MXA_OK;
   if (a.rows * a.nb >= ((int64_t)1 << 30)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices (x2 lanes)
-  hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (a.dt == kF16) hipLaunchKernelGGL(rows_prep_kernel<kF16>, grid, dim3(256), 0, stream, a);
+  else if (a.dt == kBF16) hipLaunchKernelGGL(rows_prep_kernel<kBF16>, grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(rows_prep_kernel<kF32>, grid, dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 int launch_elsa_prep(const ElsaPrepArgs& a, hipStream_t stream) {
@@ -399,18 +445,24 @@ int launch_attn_prep(const RowsPrepArgs& q, const RowsPrepArgs& k, const ColsPre
   if (q.rows * q.nb >= ((int64_t)1 << 30) || k.rows * k.nb >= ((int64_t)1 << 30) ||
       v.mats * v.nb * v.C >= ((int64_t)1 << 31))
     return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices
+  if (q.dt != k.dt || q.dt != v.dt) return MXA_ERR_ARG;
   const int64_t nq = (q.rows * q.nb * 2 + 255) / 256, nk = (k.rows * k.nb * 2 + 255) / 256;
   const int64_t nv = (v.mats * v.nb * v.C + 255) / 256;
   if (nq + nk + nv == 0) return MXA_OK;
-  hipLaunchKernelGGL(attn_prep_kernel, dim3((unsigned)(nq + nk + nv)), dim3(256), 0, stream, q, k, v, (uint32_t)nq,
-                     (uint32_t)nk);
+  const dim3 grid((unsigned)(nq + nk + nv));
+  if (q.dt == kF16) hipLaunchKernelGGL(attn_prep_kernel<kF16>, grid, dim3(256), 0, stream, q, k, v, (uint32_t)nq, (uint32_t)nk);
+  else if (q.dt == kBF16) hipLaunchKernelGGL(attn_prep_kernel<kBF16>, grid, dim3(256), 0, stream, q, k, v, (uint32_t)nq, (uint32_t)nk);
+  else hipLaunchKernelGGL(attn_prep_kernel<kF32>, grid, dim3(256), 0, stream, q, k, v, (uint32_t)nq, (uint32_t)nk);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 int launch_cols_prep(const ColsPrepArgs& a, hipStream_t stream) {
   const int64_t threads = a.mats * a.nb * a.C;
   if (threads == 0) return MXA_OK;
   if (threads >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;  // 32-bit thread indices
-  hipLaunchKernelGGL(cols_prep_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (a.dt == kF16) hipLaunchKernelGGL(cols_prep_kernel<kF16>, grid, dim3(256), 0, stream, a);
+  else if (a.dt == kBF16) hipLaunchKernelGGL(cols_prep_kernel<kBF16>, grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(cols_prep_kernel<kF32>, grid, dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 }  // namespace mxa

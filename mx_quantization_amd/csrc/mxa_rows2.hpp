@@ -31,10 +31,12 @@ struct Rows2Args {
   int B, H, N, T, D, nbd, dpad, ntb, tpad;
   int kst, vst;  // LDS row strides of the K code tables and the V^T table
   int k_top, bfloat, flush_p;
+  int in_dt;  // dtype of q, k, v and the bias (MXA_DT_*)
+  int s_dt;   // dtype of the scores, P and the output (the GEMM outputs: include/mxa.h score_dtype)
   float scale;
-  const float* bias;
+  const void* bias;  // dtype in_dt
   int64_t bs0, bs1, bs2, bs3;
-  float* out;
+  void* out;  // dtype s_dt
   int64_t os0, os1, os2;
   int64_t* idx_out;
   float* true_out;
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
   const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
   for (int r = (int)blockIdx.y * a.rows_per_wg + __builtin_amdgcn_readfirstlane(wave); r < r_end; r += a.waves) {
     const int64_t grow = (int64_t)bh * a.N + r;
-    const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : nullptr;
+    const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : -1;
     const int8_t* qmx = a.qc + grow * a.dpad;
 
     // ---- the row's T true scores in position order ----------------------------
@@ -157,13 +159,14 @@ __global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
       bool nan = false;
       const double acc = r2_dot<0>(qmx, a.qsT, grow * nbd, nbd, tmx + (size_t)j * kst, tsT + j * nbd, nan);
       // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
-      vals[s] = round_bfloat(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.bfloat, kRoundNearest, 1) * a.scale;
+      vals[s] = round_dt(round_bfloat(round_dt(nan ? __uint_as_float(0x7FC00000u) : (float)acc, a.s_dt), a.bfloat,
+                                      kRoundNearest, 1, a.s_dt) * a.scale, a.s_dt);
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int j = 64 * s + lane;
       if (j < T) {
-        if (brow) vals[s] = vals[s] + brow[(int64_t)j * a.bs3];
+        if (brow >= 0) vals[s] = round_dt(vals[s] + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
         if (a.true_out) a.true_out[grow * T + j] = vals[s];
       }
     }
@@ -190,14 +193,14 @@ __global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
     for (int s = 0; s < S; ++s) {
       const int pos = s * 64 + lane;
       if (s * 64 >= a.tpad) break;
-      const float x = round_bfloat(vals[s] / sum, a.bfloat, kRoundNearest, 1);
+      const float x = round_dt(round_bfloat(vals[s] / sum, a.bfloat, kRoundNearest, 1, a.s_dt), a.s_dt);
       const uint32_t mb = half_reduce(__float_as_uint(x) & 0x7FFFFFFFu,
                                       [](uint32_t u, uint32_t w) { return u > w ? u : w; });
       int e_raw;
-      const int es = scale_exponent(mb, 127, &e_raw);
+      const int es = scale_exponent_dt(mb, 127, a.s_dt, &e_raw);
       float xv = x;
       if (a.flush_p && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
-      const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+      const int code = es == kExpNaN ? 0 : (int)round_code(xv, es, 8, kRoundNearest, a.s_dt);
       if (pos < a.tpad) {
         prow[pos] = (int8_t)code;
         if ((lane & 31) == 0) pe[pos >> 5] = es == kExpNaN ? kExpNaN : es - 6;
@@ -241,7 +244,8 @@ __global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
         const int d = 64 * ds + lane;
         if (ds < dsl && d < D) {
           const float o = nan[ds] ? __uint_as_float(0x7FC00000u) : (float)acc[ds];
-          a.out[b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + d] = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+          store_dt(a.out, b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + d,
+                   round_bfloat(round_dt(o, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt), a.s_dt);
         }
       }
     }

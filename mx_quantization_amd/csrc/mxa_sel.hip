@@ -83,9 +83,10 @@ static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t str
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
-extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
-                        float* out_vals, uint32_t* out_mask, hipStream_t stream) {
+extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
+                        void* out_vals, uint32_t* out_mask, int32_t dtype, hipStream_t stream) {
   if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
+  if (dtype != kF32 && dtype != kF16 && dtype != kBF16) return MXA_ERR_ARG;
   if (n > 512) return MXA_ERR_UNSUPPORTED;
   if (rows == 0) return MXA_OK;
   if (k == 0) {
@@ -93,7 +94,7 @@ extern "C" int mxa_topk(const float* vals, int64_t rows, int32_t n, int64_t ld, 
                              ? MXA_OK : MXA_ERR_LAUNCH;
     return MXA_OK;
   }
-  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask};
+  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
   const unsigned grid = (unsigned)((rows + 15) / 16);
   if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
   if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);

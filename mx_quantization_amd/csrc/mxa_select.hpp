@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
     const int r = rq + gi;
     const bool valid = r < r_end;
     const int64_t grow = (int64_t)bh * a.N + (valid ? r : rq);
-    const float* brow = a.bias ? a.bias + b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : rq) * a.bs2 : nullptr;
+    const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : rq) * a.bs2 : -1;
 
     // ---- the row's scores into its mirror ------------------------------------
 #ifdef MXA_SEL_SKIP
@@ -231,8 +231,11 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
 #else
     if (valid) {
 #endif
+      // scores in the score dtype: the approximator GEMM's (or the true matmul's) output
+      // rounded to it, then + bias (MX_transformer_block.py:821-822), rounded again
       auto emit = [&](int j, float v) {
-        if (brow) v = v + brow[(int64_t)j * a.bs3];
+        v = round_dt(v, a.s_dt);
+        if (brow >= 0) v = round_dt(v + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
         if (MODE == kModeTrue) {
           if (a.true_out) a.true_out[grow * T + j] = v;
         } else if (a.pred_out) {
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
         }
         auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
           constexpr int NBD = decltype(nbd_c)::value;
-          if (brow) {
+          if (brow >= 0 || a.s_dt != kF32) {
             for (int j = gl; j < T; j += 16) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
             return;
           }
@@ -343,7 +346,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
             acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
           float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
           // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
-          if (MODE == kModeTrue) v = round_bfloat(v, a.bfloat, kRoundNearest, 1) * a.scale;
+          if (MODE == kModeTrue) v = round_bfloat(round_dt(v, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt) * a.scale;
           emit(j, v);
         }
       }
@@ -390,12 +393,13 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
 
 // ---- standalone top-k over rows of a float matrix (mxa_topk) ------------------
 struct GrpTopkArgs {
-  const float* vals;
+  const void* vals;  // dtype dt
   int64_t rows, ld;
   int n, k;
   int64_t* out_idx;
-  float* out_vals;
+  void* out_vals;  // dtype dt
   uint32_t* out_mask;
+  int dt;
 };
 
 template <int NP>
@@ -406,16 +410,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
   const bool valid = row < a.rows;
   const int npa = grp_alloc(a.n);
   const GrpRow g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
-  const float* src = a.vals + (valid ? row : 0) * a.ld;
+  const int64_t src = (valid ? row : 0) * a.ld;
   if (valid)
-    for (int j = gl; j < a.n; j += 16) g.A[j] = pack_ki(order_key(src[j]), (uint32_t)j);
+    for (int j = gl; j < a.n; j += 16) g.A[j] = pack_ki(order_key(load_dt(a.vals, src + j, a.dt)), (uint32_t)j);
   wave_lds_sync();
   grp_topk<NP>(g, a.n, a.k, valid, gl);
   if (valid) {
     for (int p = gl; p < a.k; p += 16) {
       const uint32_t ix = (uint32_t)g.A[p];
       a.out_idx[row * a.k + p] = (int64_t)ix;
-      if (a.out_vals) a.out_vals[row * a.k + p] = src[ix];
+      if (a.out_vals) store_dt(a.out_vals, row * a.k + p, load_dt(a.vals, src + ix, a.dt), a.dt);
     }
   }
   if (a.out_mask) {

@@ -30,8 +30,10 @@ class exponent_approximation:
             raise NotImplementedError("approximators are built for 32-element MX blocks")
         if mx_specs["round_mx_output"] != "nearest":
             raise NotImplementedError("approximators are built for round_mx_output='nearest'")
-        self.Q = quantize_elemwise_op(Q, mx_specs, round=mx_specs["round_output"]).float()
-        self.K = quantize_elemwise_op(K, mx_specs, round=mx_specs["round_output"]).float()
+        # the operands keep their dtype: the reference's ops follow it (float16 / bfloat16
+        # inputs quantize by that dtype's rules, include/mxa.h MXA_DT_*)
+        self.Q = quantize_elemwise_op(Q, mx_specs, round=mx_specs["round_output"])
+        self.K = quantize_elemwise_op(K, mx_specs, round=mx_specs["round_output"])
         self.shared_exponent_method = mx_specs.get("shared_exp_method", "max")
         self._flush = bool(mx_specs["mx_flush_fp32_subnorms"])
         # MXINT8 copies (funcs/exponent_based_prediction.py:18-31)

@@ -2,9 +2,10 @@
 
 out = MX(x, along in_features) @ MX(W, along in_features)^T (+ bias), on the
 device through mxa_matmul.  This is the qkv / proj projection around the
-attention core (a SURVEY §8f "next" row): present so the patched modules'
-`from mx import Linear` keeps working; its fusion into the attention kernels is
-future work."""
+attention core (a SURVEY §8f "next" row): the unfused drop-in, so the patched
+modules' `from mx import Linear` keeps working.  The fused forms are
+mx_quantization_amd.mx_qkv_attention (qkv Linear -> attention operands) and the
+proj Linear on the attention output (include/mxa.h)."""
 from __future__ import annotations
 
 import torch
@@ -21,16 +22,17 @@ def linear(input, weight, bias=None, mx_specs=None, prequantized_weights=False, 
         return torch.nn.functional.linear(input, weight, bias)
     s = apply_mx_specs(mx_specs)
     _check_specs(s)
-    bf_in = quantize_elemwise_op(input, mx_specs=s, round=s["round_output"]).float()
-    bf_w = weight.float() if prequantized_weights else quantize_elemwise_op(weight, mx_specs=s,
-                                                                             round=s["round_weight"]).float()
+    bf_in = quantize_elemwise_op(input, mx_specs=s, round=s["round_output"])
+    bf_w = weight if prequantized_weights else quantize_elemwise_op(weight, mx_specs=s, round=s["round_weight"])
     x2 = bf_in.reshape(1, -1, bf_in.shape[-1])
+    # f_linear under torch.autocast returns the autocast dtype (then + the fp32 bias
+    # promotes to fp32, linear.py:88-101); outside it the operands' dtypes must agree
     out = ops.mx_matmul(x2, bf_w.t().unsqueeze(0), _mbits(s["a_elem_format"]), _mbits(s["w_elem_format"]),
-                        flush=s["mx_flush_fp32_subnorms"])
+                        flush=s["mx_flush_fp32_subnorms"], out_dtype=ops.autocast_dtype(x2.device.type))
     out = out.reshape(bf_in.shape[:-1] + (weight.shape[0],))
     out = quantize_elemwise_op(out, mx_specs=s, round=s["round_output"])
     if bias is not None:
-        bb = bias.float() if prequantized_weights else quantize_elemwise_op(bias, mx_specs=s, round=s["round_weight"])
+        bb = bias if prequantized_weights else quantize_elemwise_op(bias, mx_specs=s, round=s["round_weight"])
         out = quantize_elemwise_op(out + bb, mx_specs=s, round=s["round_output"])
     return out
 

@@ -44,7 +44,11 @@ def matmul(in1, in2, bias=None, mx_specs=None, name=None, mode_config="aa"):
     if f1 is None or f2 is None:
         raise NotImplementedError("mx.matmul with an unquantized operand")
     _check_specs(s)
-    out = ops.mx_matmul(bf1.float(), bf2.float(), _mbits(f1), _mbits(f2), flush=s["mx_flush_fp32_subnorms"])
+    # each operand is quantized in its own dtype; torch_matmul returns the autocast dtype
+    # under torch.autocast (P float16 @ V float32 in the autocast DeiT eval), else the
+    # operands' common dtype (mismatched dtypes raise, as torch.matmul does)
+    out = ops.mx_matmul(bf1, bf2, _mbits(f1), _mbits(f2), flush=s["mx_flush_fp32_subnorms"],
+                        out_dtype=ops.autocast_dtype(bf1.device.type))
     out = quantize_elemwise_op(out, mx_specs=s, round=s["round_output"])
     if bias is not None:
         out = out + quantize_elemwise_op(bias, mx_specs=s, round=s["round_weight"])

@@ -29,6 +29,22 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
     return t
 
 
+def _dt(t: torch.Tensor, name: str) -> int:
+    """MXA_DT_* of a float32 / float16 / bfloat16 tensor.  The kernels read the tensor in
+    its own dtype and follow the reference's dtype rules (include/mxa.h MXA_DT_*)."""
+    try:
+        return N.DTYPES[t.dtype]
+    except KeyError:
+        raise TypeError(f"{name} must be float32, float16 or bfloat16 (got {t.dtype})") from None
+
+
+def autocast_dtype(device_type: str = "cuda"):
+    """torch.autocast's lower-precision dtype when it is enabled for `device_type`, else None."""
+    if torch.is_autocast_enabled(device_type):
+        return torch.get_autocast_dtype(device_type)
+    return None
+
+
 def _split(shape, axis):
     axis = axis % len(shape) if len(shape) else 0
     outer = 1
@@ -45,7 +61,8 @@ def quantize_mx(A: torch.Tensor, elem_mbits: int = 8, block_size: int = 32, axis
     """MX block quantization along one axis (mx_ops.py:180-306).  Returns the
     dequantized tensor, plus (codes int8, block exponents int16) if want_codes."""
     dev = require_device(A)
-    A = _f32(A, "A").contiguous()
+    dt = _dt(A, "A")
+    A = A.contiguous()
     y = torch.empty_like(A)
     outer, L, inner = _split(tuple(A.shape), axis)
     codes = exps = None
@@ -56,7 +73,7 @@ def quantize_mx(A: torch.Tensor, elem_mbits: int = 8, block_size: int = 32, axis
     if A.numel():
         check(lib().mxa_quantize_mx(A.data_ptr(), y.data_ptr(), codes.data_ptr() if want_codes else None,
                                     exps.data_ptr() if want_codes else None, outer, L, inner, block_size,
-                                    elem_mbits, scale_bits, N.ROUND_MODES[round], int(flush), int(bfloat),
+                                    elem_mbits, scale_bits, N.ROUND_MODES[round], int(flush), int(bfloat), dt,
                                     stream_ptr(dev)), "mxa_quantize_mx")
     return (y, codes, exps) if want_codes else y
 
@@ -66,7 +83,8 @@ def shared_exponents(A: torch.Tensor, method: str = "max", axis: int = -1, block
     """_shared_exponents (mx_ops.py:49-99) for one axis; 'max' keeps the axis as
     the block count (size 1 when block_size covers the axis)."""
     dev = require_device(A)
-    A = _f32(A, "A").contiguous()
+    dt = _dt(A, "A")
+    A = A.contiguous()
     outer, L, inner = _split(tuple(A.shape), axis)
     if method == "none":
         out = torch.empty_like(A)
@@ -75,12 +93,12 @@ def shared_exponents(A: torch.Tensor, method: str = "max", axis: int = -1, block
         bs = L if block_size == 0 else block_size
         shape = list(A.shape)
         shape[axis % A.dim()] = (L + bs - 1) // bs
-        out = torch.empty(shape, dtype=torch.float32, device=dev)
+        out = torch.empty(shape, dtype=A.dtype, device=dev)
         m = 0
     else:
         raise ValueError(f"Unrecognized shared exponent selection method {method}")
     if A.numel():
-        check(lib().mxa_shared_exponents(A.data_ptr(), out.data_ptr(), outer, L, inner, block_size, m, ebits,
+        check(lib().mxa_shared_exponents(A.data_ptr(), out.data_ptr(), outer, L, inner, block_size, m, ebits, dt,
                                          stream_ptr(dev)), "mxa_shared_exponents")
     return out
 
@@ -88,11 +106,12 @@ def shared_exponents(A: torch.Tensor, method: str = "max", axis: int = -1, block
 def quantize_bfloat(A: torch.Tensor, bfloat: int = 16, round: str = "nearest", allow_denorm: bool = True):
     """bfloatX elementwise quantization (elemwise_ops.py:201-216)."""
     dev = require_device(A)
-    A = _f32(A, "A").contiguous()
+    dt = _dt(A, "A")
+    A = A.contiguous()
     y = torch.empty_like(A)
     if A.numel():
         check(lib().mxa_quantize_bfloat(A.data_ptr(), y.data_ptr(), A.numel(), int(bfloat), N.ROUND_MODES[round],
-                                        int(allow_denorm), stream_ptr(dev)), "mxa_quantize_bfloat")
+                                        int(allow_denorm), dt, stream_ptr(dev)), "mxa_quantize_bfloat")
     return y
 
 
@@ -103,13 +122,14 @@ OP_KINDS = {"sign": N.MXA_OP_SIGN, "mxint8": N.MXA_OP_MXINT8, "mxint4": N.MXA_OP
 def approx_values(X: torch.Tensor, kind: str, flush: bool = False, bfloat: int = 0) -> torch.Tensor:
     """Approximator operand values along the last axis (funcs/exponent_based_prediction.py)."""
     dev = require_device(X)
-    X = _f32(X, "X").contiguous()
+    dt = _dt(X, "X")
+    X = X.contiguous()
     out = torch.empty_like(X)
     d = X.shape[-1]
     rows = X.numel() // d if d else 0
     if rows:
         check(lib().mxa_approx_values(X.data_ptr(), out.data_ptr(), rows, d, d, d, OP_KINDS[kind], int(flush),
-                                      int(bfloat), stream_ptr(dev)), "mxa_approx_values")
+                                      int(bfloat), dt, stream_ptr(dev)), "mxa_approx_values")
     return out
 
 
@@ -118,15 +138,16 @@ def topk(vals: torch.Tensor, k: int, return_mask: bool = False):
     index order (TopKImpl.h:45-86), computed on the device.  Returns (values, idx),
     plus the prune mask as packed words (..., ceil(n/32)) int32 if return_mask."""
     dev = require_device(vals)
-    vals = _f32(vals, "vals").contiguous()
+    dt = _dt(vals, "vals")
+    vals = vals.contiguous()
     n = vals.shape[-1]
     rows = vals.numel() // n if n else 0
     idx = torch.empty(vals.shape[:-1] + (k,), dtype=torch.int64, device=dev)
-    out = torch.empty(vals.shape[:-1] + (k,), dtype=torch.float32, device=dev)
+    out = torch.empty(vals.shape[:-1] + (k,), dtype=vals.dtype, device=dev)
     mask = torch.empty(vals.shape[:-1] + ((n + 31) // 32,), dtype=torch.int32, device=dev) if return_mask else None
     if rows:
         check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(),
-                             mask.data_ptr() if return_mask else None, stream_ptr(dev)), "mxa_topk")
+                             mask.data_ptr() if return_mask else None, dt, stream_ptr(dev)), "mxa_topk")
     return (out, idx, mask) if return_mask else (out, idx)
 
 
@@ -138,11 +159,18 @@ def unpack_mask(words: torch.Tensor, n: int) -> torch.Tensor:
 
 
 def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbits_b: int = 8, flush: bool = False,
-              bfloat: int = 0) -> torch.Tensor:
-    """MX matmul forward (matmul.py:31-100): a (..., M, K) along K, b (..., K, Nc) along K."""
+              bfloat: int = 0, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """MX matmul forward (matmul.py:31-100): a (..., M, K) along K, b (..., K, Nc) along K.
+    Each operand is quantized in its own dtype; the product is rounded once to out_dtype
+    (default: the operands' dtype, which must then agree -- torch.matmul's rule; under
+    torch.autocast the caller passes the autocast dtype)."""
     dev = require_device(a, b)
-    a = _f32(a, "in1")
-    b = _f32(b, "in2")
+    adt, bdt = _dt(a, "in1"), _dt(b, "in2")
+    if out_dtype is None:
+        if a.dtype != b.dtype:
+            raise RuntimeError(f"expected both operands to have the same dtype, got {a.dtype} and {b.dtype}")
+        out_dtype = a.dtype
+    cdt = N.DTYPES[out_dtype]
     if a.dim() < 2 or b.dim() < 2:
         raise ValueError("mx matmul needs >= 2-D operands")
     batch_shape = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
@@ -155,7 +183,7 @@ def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbit
     batch = 1
     for s in batch_shape:
         batch *= s
-    c = torch.empty(batch_shape + (M, Nc), dtype=torch.float32, device=dev)
+    c = torch.empty(batch_shape + (M, Nc), dtype=out_dtype, device=dev)
     if batch == 0 or M == 0 or Nc == 0:
         return c
     if K == 0:
@@ -163,8 +191,8 @@ def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbit
     nbytes = lib().mxa_matmul_workspace_bytes(batch, M, K, Nc)
     ws = _workspace(dev, nbytes)
     check(lib().mxa_matmul(a.data_ptr(), b.data_ptr(), c.data_ptr(), batch, M, K, Nc, M * K, K * Nc, elem_mbits_a,
-                           elem_mbits_b, int(flush), int(bfloat), ws.data_ptr(), ws.numel(), stream_ptr(dev)),
-          "mxa_matmul")
+                           elem_mbits_b, int(flush), int(bfloat), adt, bdt, cdt, ws.data_ptr(), ws.numel(),
+                           stream_ptr(dev)), "mxa_matmul")
     return c
 
 
@@ -186,10 +214,24 @@ def elsa_cos_table(d: int) -> torch.Tensor:
     return torch.cos(torch.clamp(est - 0.127, min=0))
 
 
-def _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx, bias, flush_subnormals, bfloat, elsa_proj):
+def _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx, bias, flush_subnormals, bfloat, elsa_proj,
+                 autocast=None):
+    """autocast: None, or the torch.autocast dtype (float16 / bfloat16) under which the
+    reference's matmuls return that dtype (include/mxa.h score_dtype)."""
     dev = require_device(q, k, v, bias, elsa_proj)
-    for t, nm in ((q, "q"), (k, "k")) + (((v, "v"),) if v is not None else ()):
-        _f32(t, nm)
+    dt = _dt(q, "q")
+    for t, nm in ((k, "k"),) + (((v, "v"),) if v is not None else ()):
+        if t.dtype != q.dtype:
+            raise TypeError(f"{nm} must have q's dtype {q.dtype} (got {t.dtype})")
+    sdt = 0
+    if autocast is not None and autocast != torch.float32:
+        if autocast not in (torch.float16, torch.bfloat16):
+            raise TypeError(f"autocast dtype must be float16 or bfloat16 (got {autocast})")
+        sdt = N.DTYPES[autocast]
+    if approx and pred_mode == "ELSA" and bias is not None:
+        # elsa_approximation.approximation_scores adds no bias (deit main.py:120-121, DiT
+        # models.py:188-189, PixArt :676-677): ranking ELSA scores plus a bias would differ
+        raise ValueError("pred_mode 'ELSA' takes no bias: the reference's ELSA scores are unbiased")
     B, H, Nq, D = q.shape
     Bk, Hk, T, Dk = k.shape
     if (Bk, Hk, Dk) != (B, H, D) or (v is not None and tuple(v.shape) != (B, H, T, D)):
@@ -214,8 +256,10 @@ def _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx, bias, flush_su
     p.pred_mode = N.PRED_MODES.get(pred_mode, 0)
     p.top_k, p.approx = int(bool(top_k)), int(bool(approx))
     p.flush_subnormals, p.bfloat = int(bool(flush_subnormals)), int(bfloat)
+    p.dtype, p.score_dtype = dt, sdt
     if bias is not None:
-        _f32(bias, "bias")
+        if bias.dtype != q.dtype:
+            raise TypeError(f"bias must have q's dtype {q.dtype} (got {bias.dtype})")
         bias4 = bias
         while bias4.dim() < 4:
             bias4 = bias4.unsqueeze(0)
@@ -241,18 +285,29 @@ def _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx, bias, flush_su
     return p, dev, (B, H, Nq, T, D), keep
 
 
+def _out_dtype(q, autocast):
+    return autocast if autocast in (torch.float16, torch.bfloat16) else q.dtype
+
+
 def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, k_top: int = 20,
                       pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
                       bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
                       return_scores: bool = False, out: Optional[torch.Tensor] = None,
-                      return_mask: bool = False, elsa_proj: Optional[torch.Tensor] = None):
+                      return_mask: bool = False, elsa_proj: Optional[torch.Tensor] = None,
+                      autocast: Optional[torch.dtype] = None):
     """The fused hot path (include/mxa.h mxa_attention): q (B,H,N,D), k/v (B,H,T,D)
-    float32 (strided views of a packed qkv are fine).  Returns (out (B,H,N,D),
-    idx (B,H,N,k_top) int64 or None[, true, pred][, mask words (B,H,N,ceil(T/32))])."""
+    float32, float16 or bfloat16 (strided views of a packed qkv are fine; the ops follow
+    the tensors' dtype as the reference's do).  autocast: the torch.autocast dtype the
+    reference's matmuls would return (scores, P and out in it).  Returns (out (B,H,N,D),
+    idx (B,H,N,k_top) int64 or None[, true, pred][, mask words (B,H,N,ceil(T/32))]);
+    true / pred are float32 tensors holding the score-dtype values."""
     p, dev, (B, H, Nq, T, D), keep = _attn_params(q, k, v, scale, k_top, pred_mode, top_k, approx and top_k, bias,
-                                                  flush_subnormals, bfloat, elsa_proj)
+                                                  flush_subnormals, bfloat, elsa_proj, autocast)
+    odt = _out_dtype(q, autocast)
     if out is None:
-        out = torch.empty((B, H, Nq, D), dtype=torch.float32, device=dev)
+        out = torch.empty((B, H, Nq, D), dtype=odt, device=dev)
+    elif out.dtype != odt:
+        raise TypeError(f"out must be {odt} (got {out.dtype})")
     p.out = out.data_ptr()
     p.out_strides[:] = (out.stride(0), out.stride(1), out.stride(2))
     if out.stride(3) != 1:
@@ -282,18 +337,19 @@ def mx_topk_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: 
 
 def mx_approx_scores(q: torch.Tensor, k: torch.Tensor, pred_mode: str = "ex_pred",
                      bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False, bfloat: int = 0,
-                     elsa_proj: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     elsa_proj: Optional[torch.Tensor] = None, autocast: Optional[torch.dtype] = None) -> torch.Tensor:
     """pred = aQ @ aK^T (+ bias) of the approximator `pred_mode` (or ELSA's
-    approximation_scores), (B,H,N,T) float32 -- include/mxa.h mxa_approx_scores."""
+    approximation_scores), (B,H,N,T) in the score dtype -- include/mxa.h mxa_approx_scores."""
     p, dev, (B, H, Nq, T, D), keep = _attn_params(q, k, None, 1.0, 0, pred_mode, False, True, bias,
-                                                  flush_subnormals, bfloat, elsa_proj)
+                                                  flush_subnormals, bfloat, elsa_proj, autocast)
     pred = torch.empty((B, H, Nq, T), dtype=torch.float32, device=dev)
     p.pred_out = pred.data_ptr()
     nbytes = lib().mxa_attention_workspace_bytes(ctypes.byref(p))
     ws = _workspace(dev, nbytes)
     p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
     check(lib().mxa_approx_scores(ctypes.byref(p), stream_ptr(dev)), "mxa_approx_scores")
-    return pred
+    odt = _out_dtype(q, autocast)
+    return pred if odt == torch.float32 else pred.to(odt)  # the values are exact in odt
 
 
 class LinearWeightMX:
@@ -320,10 +376,13 @@ class LinearWeightMX:
 def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_heads: int, scale: float,
                      k_top: int = 20, pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
                      flush_subnormals: bool = False, bfloat: int = 0, return_qkv: bool = False,
-                     elsa_proj: Optional[torch.Tensor] = None):
+                     elsa_proj: Optional[torch.Tensor] = None, autocast: Optional[torch.dtype] = None):
     """The qkv mx.Linear fused into the attention core (include/mxa.h mxa_qkv_attention):
     x (B, N, C) float32 tokens; weight a (3C', C) tensor or a LinearWeightMX; returns
-    (out (B,H,N,D), idx (B,H,N,k) or None[, qkv (B,N,3C') fp32 projection])."""
+    (out (B,H,N,D), idx (B,H,N,k) or None[, qkv (B,N,3C') fp32 projection]).
+    autocast (float16 / bfloat16): torch.autocast around the module -- the projection's
+    product is rounded to it before the fp32 bias add, and the attention's matmuls return
+    it (the output is of that dtype)."""
     dev = require_device(x, bias, elsa_proj)
     x = _f32(x, "x")
     if x.dim() != 3 or x.stride(2) != 1:
@@ -346,15 +405,16 @@ def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_
     # q / k / v are produced inside the call: stand-in views carry the shapes only
     shape_q = torch.empty((D,), device=dev).as_strided((B, num_heads, Ntok, D), (0, 0, 0, 1))
     p, _, _, keep = _attn_params(shape_q, shape_q, shape_q, scale, k_top, pred_mode, top_k, approx and top_k, None,
-                                 flush_subnormals, bfloat, elsa_proj)
+                                 flush_subnormals, bfloat, elsa_proj, autocast)
     p.q = p.k = p.v = None
-    out = torch.empty((B, num_heads, Ntok, D), dtype=torch.float32, device=dev)
+    out = torch.empty((B, num_heads, Ntok, D), dtype=_out_dtype(x, autocast), device=dev)
     p.out = out.data_ptr()
     p.out_strides[:] = (out.stride(0), out.stride(1), out.stride(2))
     idx = torch.empty((B, num_heads, Ntok, k_top), dtype=torch.int64, device=dev) if top_k else None
     p.idx_out = idx.data_ptr() if idx is not None else None
     xp = N.QkvParams()
     xp.x, xp.x_row_stride, xp.C, xp.wq = x.data_ptr(), x.stride(1), C, wq.buf.data_ptr()
+    xp.autocast_dtype = p.score_dtype
     if B > 1 and x.stride(0) != Ntok * x.stride(1):
         raise ValueError("x rows must be evenly strided over (B, N)")
     if bias is not None:

@@ -58,6 +58,45 @@ def floor_log2_f32(x: np.ndarray) -> np.ndarray:
         return np.floor(np.log2(x.astype(F64)).astype(F32)).astype(F32)
 
 
+def floor_log2_dtype(bits: np.ndarray, dtype: str) -> np.ndarray:
+    """torch.floor(torch.log2(x)) for float16 / bfloat16 x >= 0 given as uint16 bit
+    patterns, as float64 (-inf for a float16 zero: mx_ops.py:85's FP32_MIN_NORMAL
+    underflows to 0 in float16; bfloat16 zero -> -126 like float32).
+
+    log2 is rounded to the dtype: it reaches the next integer for the top `gap`
+    mantissa codes of a binade, gap depending on the octave of the exponent (float16:
+    0, 1, 2, 5; bfloat16: 0, 1, 2, 5, 10, 21, 40), and for dtype subnormals from a
+    per-leading-bit threshold.  The same rule as mxa_common.hpp floor_log2_dt; pinned
+    against torch by tests/test_oracle_golden.py on every value (dtype_exp in
+    tests/golden/attn_dtype.npz)."""
+    b = np.asarray(bits, dtype=np.uint16).astype(np.int64) & 0x7FFF
+    if dtype == "f16":
+        mb, bias, gaps = 10, 15, (0, 1, 2, 5)
+        sub_thr = {7: 255, 8: 511, 9: 1022}
+        inf_bits = 0x7C00
+    else:
+        mb, bias, gaps = 7, 127, (0, 1, 2, 5, 10, 21, 40)
+        sub_thr = {1: 3, 2: 6, 3: 12, 4: 23, 5: 54, 6: 108}
+        inf_bits = 0x7F80
+    out = np.zeros(b.shape, dtype=F64)
+    for i, v in np.ndenumerate(b):
+        E, M = int(v) >> mb, int(v) & ((1 << mb) - 1)
+        if v >= inf_bits:
+            out[i] = np.inf if v == inf_bits else np.nan
+        elif v == 0:
+            out[i] = -np.inf if dtype == "f16" else -126.0
+        elif E:
+            e = E - bias
+            u = e if e >= 0 else -e - 1
+            o = u.bit_length() - 1 if u >= 2 else 0
+            out[i] = e + (1 if M + gaps[o] >= (1 << mb) else 0)
+        else:
+            j = M.bit_length() - 1
+            e = (1 - bias - mb) + j
+            out[i] = e + (1 if M >= sub_thr.get(j, 2 << j) else 0)
+    return out
+
+
 def _pow2(e: np.ndarray) -> np.ndarray:
     """2**e for float32 e holding integers or NaN (torch `2 ** tensor`)."""
     e = np.asarray(e, dtype=F32)

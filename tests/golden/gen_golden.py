@@ -370,7 +370,121 @@ def gen_topk_ties():
     print("wrote topk_ties")
 
 
+def _bits(t):
+    """float16 / bfloat16 tensor -> its uint16 bit patterns (numpy holds no bfloat16)."""
+    return t.contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _f32(t):
+    return t.float().numpy()  # exact: every float16 / bfloat16 value is a float32
+
+
+def gen_dtype():
+    """float16 / bfloat16 inputs (the reference's ops follow their input's dtype:
+    mx_ops.py:85, :283, elemwise_ops.py:146) and torch.autocast around the attention
+    glue (deit engine.py:97): exhaustive shared exponents, MX quantize KATs incl. the
+    float16 zero-block NaN, attention cases, mx.matmul, and the autocast qkv chain."""
+    from mx.mx_ops import quantize_mx_op
+    out = {}
+    s = specs()
+    for name, dt, lim in (("f16", torch.float16, 0x7C00), ("bf16", torch.bfloat16, 0x7F80)):
+        # every positive finite value: floor(log2(x)) in the dtype (method 'none')
+        u = torch.arange(0, lim, dtype=torch.int32).to(torch.int16)
+        x = u.view(dt)
+        out[f"{name}/sexp_x"] = _bits(x)
+        out[f"{name}/sexp_none"] = _f32(_shared_exponents(x, method="none"))
+        # quantize KATs: random blocks + specials (zero block, tiny, large, inf/nan), both axes
+        rng = np.random.default_rng(5)
+        a = rng.standard_normal((6, 96), dtype=np.float32) * np.float32(3.0)
+        a[1, 32:64] = 0.0                        # all-zero block
+        a[2, :32] *= np.float32(2.0 ** -20)      # tiny block (float16 subnormals)
+        a[3, 64:] *= np.float32(2.0 ** 10)       # large block
+        a[4, 5] = np.inf
+        a[5, 40] = np.nan
+        a[0, :32] = np.linspace(-1, 1, 32, dtype=np.float32) * np.float32(1.9921875)
+        at = torch.from_numpy(a).to(dt)
+        out[f"{name}/q_x"] = _bits(at)
+        out[f"{name}/q_int8_ax1"] = _f32(quantize_mx_op(at, s, elem_format="int8", axes=[-1]))
+        out[f"{name}/q_int4_ax1"] = _f32(quantize_mx_op(at, s, elem_format="int4", axes=[-1]))
+        out[f"{name}/q_int8_ax0"] = _f32(quantize_mx_op(at, s, elem_format="int8", axes=[-2]))
+        out[f"{name}/q_int8_flush"] = _f32(quantize_mx_op(at, specs(mx_flush_fp32_subnorms=True),
+                                                          elem_format="int8", axes=[-1]))
+        # the attention glue on dtype tensors (DeiT-tiny, DiT slice)
+        for tag, shp, k_top, modes in (("deit", (1, 3, 197, 64), 20, ("ex_pred", "MXINT4", "partial_Q")),
+                                       ("dit", (1, 2, 256, 72), 154, ("ex_pred",))):
+            q = torch.from_numpy(rnd(shp, 20)).to(dt)
+            kk = torch.from_numpy(rnd(shp, 21)).to(dt)
+            v = torch.from_numpy(rnd(shp, 22)).to(dt)
+            out[f"{name}/{tag}/q"], out[f"{name}/{tag}/k"], out[f"{name}/{tag}/v"] = _bits(q), _bits(kk), _bits(v)
+            sc = shp[-1] ** -0.5
+            for mode in modes:
+                r = attention_glue_t(q, kk, v, s, sc, k_top, mode)
+                keys = ("idx", "out") if mode != "ex_pred" else (("true", "pred", "idx", "out") if tag == "deit" else
+                                                                 ("pred", "idx", "out"))
+                for key in keys:
+                    out[f"{name}/{tag}/{mode}/{key}"] = r[key]
+            out[f"{name}/{tag}/dense/out"] = attention_glue_t(q, kk, v, s, sc, k_top, "ex_pred", top_k=False)["out"]
+        # mx.matmul on dtype tensors
+        a2 = torch.from_numpy(rnd((2, 40, 72), 30)).to(dt)
+        b2 = torch.from_numpy(rnd((2, 72, 24), 31)).to(dt)
+        out[f"{name}/mm_a"], out[f"{name}/mm_b"] = _bits(a2), _bits(b2)
+        out[f"{name}/mm_c"] = _f32(mx.matmul(a2, b2, mx_specs=s, mode_config="aa"))
+        # torch.autocast around the fp32 attention (deit engine.py:97 + main.py:101-152)
+        shp = (1, 3, 197, 64)
+        q, kk, v = (torch.from_numpy(rnd(shp, sd)) for sd in (40, 41, 42))
+        out["ac/q"], out["ac/k"], out["ac/v"] = q.numpy(), kk.numpy(), v.numpy()
+        with torch.autocast("cpu", dtype=dt):
+            for mode in ("ex_pred", "MXINT4"):
+                r = attention_glue_t(q, kk, v, s, 64 ** -0.5, 20, mode)
+                for key in (("true", "pred", "idx", "out") if mode == "ex_pred" else ("idx", "out")):
+                    out[f"{name}/ac/{mode}/{key}"] = r[key]
+            out[f"{name}/ac/dense/out"] = attention_glue_t(q, kk, v, s, 64 ** -0.5, 20, "ex_pred", top_k=False)["out"]
+        # the autocast qkv chain: mx.Linear (autocast) -> split -> attention (autocast)
+        rng = np.random.default_rng(50)
+        C, H = 192, 3
+        x = torch.from_numpy(rng.standard_normal((1, 197, C), dtype=np.float32))
+        lin = mx.Linear(C, 3 * C, bias=True, mx_specs=s)
+        with torch.no_grad():
+            lin.weight.copy_(torch.from_numpy(rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(C ** -0.5)))
+            lin.bias.copy_(torch.from_numpy(rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.02)))
+            out["acq/x"], out["acq/W"], out["acq/bias"] = x.numpy(), lin.weight.numpy().copy(), lin.bias.numpy().copy()
+            with torch.autocast("cpu", dtype=dt):
+                qkv = lin(x)
+                qq, kq, vq = qkv.reshape(1, 197, 3, H, C // H).permute(2, 0, 3, 1, 4)
+                r = attention_glue_t(qq, kq, vq, s, (C // H) ** -0.5, 20, "ex_pred")
+            out[f"{name}/acq/qkv"] = qkv.numpy()
+            for key in ("idx", "out"):
+                out[f"{name}/acq/{key}"] = r[key]
+    np.savez_compressed(os.path.join(OUT, "attn_dtype.npz"), **out)
+    print("wrote attn_dtype")
+
+
+def attention_glue_t(q, k, v, s, scale, k_top, mode, top_k=True):
+    """attention_glue for float16 / bfloat16 / autocast: the same glue, outputs as float32
+    arrays of the dtype's values (idx int64)."""
+    res = {}
+    true_scores = mx.matmul(q, k.transpose(-2, -1), mx_specs=s, mode_config='aa')
+    true_scores = true_scores * scale
+    res["true"] = true_scores
+    if top_k:
+        aq, ak = approx_ops(q, k, s, mode)
+        pred = aq @ ak.transpose(-2, -1)
+        res["pred"] = pred
+        _, idx = torch.topk(pred, k_top, dim=-1, largest=True, sorted=True)
+        vals = true_scores.gather(dim=-1, index=idx)
+        res["idx"] = idx
+        attn = torch.zeros_like(true_scores)
+        attn.scatter_(-1, idx, torch.softmax(vals, dim=-1).to(attn.dtype))
+    else:
+        attn = torch.softmax(true_scores, dim=-1)
+    res["out"] = mx.matmul(attn, v, mx_specs=s, mode_config='aa')
+    # compact: idx int16, the rest as uint16 bit patterns of the 16-bit dtype (float32 when it is float32)
+    return {kk: (vv.numpy().astype(np.int16) if vv.dtype == torch.int64 else
+                 (vv.numpy() if vv.dtype == torch.float32 else _bits(vv))) for kk, vv in res.items()}
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv", "analysis"]
+    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv", "analysis",
+                             "dtype"]
     for w in which:
         globals()["gen_" + w]()

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(N.EXPORTS), "ctypes signatures out of sync with include/mxa.h"
-    assert lib.mxa_abi_version() == N.ABI_VERSION == 2
+    assert lib.mxa_abi_version() == N.ABI_VERSION == 3
 
 
 def test_status_strings_and_arg_errors():
@@ -34,10 +34,12 @@ def test_status_strings_and_arg_errors():
     lib = N.lib()
     assert lib.mxa_status_string(0) == b"ok"
     # argument validation happens before any launch, so these run without a GPU
-    assert lib.mxa_quantize_mx(None, None, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, None) == -1
-    assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 5, 8, 0, 0, 0, None) == -2  # fp formats
-    assert lib.mxa_topk(1, 1, 600, 600, 3, 1, None, None, None) == -2  # n > 512
-    assert lib.mxa_topk(1, 1, 10, 10, 11, 1, None, None, None) == -1  # k > n
+    assert lib.mxa_quantize_mx(None, None, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, 0, None) == -1
+    assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 5, 8, 0, 0, 0, 0, None) == -2  # fp formats
+    assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, 7, None) == -1  # bad dtype
+    assert lib.mxa_topk(1, 1, 600, 600, 3, 1, None, None, 0, None) == -2  # n > 512
+    assert lib.mxa_topk(1, 1, 10, 10, 11, 1, None, None, 0, None) == -1  # k > n
+    assert lib.mxa_topk(1, 1, 10, 10, 3, 1, None, None, 5, None) == -1  # bad dtype
     p = N.AttnParams()
     assert lib.mxa_attention_workspace_bytes(p) == -1
     assert lib.mxa_attention(p, None) == -1

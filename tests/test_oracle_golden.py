@@ -229,3 +229,13 @@ def test_linear_qkv_chain_vs_reference():
     same(r["pred"], d["pred"])
     same(r["idx"], d["idx"])
     assert O.normwise_rel_err(r["out"], d["out"]) <= 1e-3
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16"])
+def test_dtype_exponent_rule_matches_reference_on_every_value(dt):
+    """floor(log2) computed in float16 / bfloat16 (the reference's ops on tensors of
+    those dtypes) restated per binade, against torch on every positive finite value."""
+    d = np.load(os.path.join(G, "attn_dtype.npz"))
+    got = O.floor_log2_dtype(d[f"{dt}/sexp_x"], dt)
+    ref = d[f"{dt}/sexp_none"].astype(np.float64)
+    assert np.array_equal(got, ref)
