@@ -90,15 +90,32 @@ def parse_tokens(path, token_re):
 
 
 def mismatch_analysis(true_top20_file, pred_top60_file):
-    """Fraction of true top-k indices missing from the predicted lists, per file pair."""
-    token_re = re.compile(r"(Token\s+)(\d+):\s*(\[.*\])")
+    """Per token, the true top-k indices missing from the predicted list (analysis.py:159-191):
+    rewrites the true file with each `Token n: [...]` line replaced by `Token n: <count>:
+    [missing, in true order]` (other lines kept), into ./mismatch_idx.txt, and returns
+    that path.  Blocks / heads advance at token 255 / head 15 as in parse_tokens."""
+    true_top20_file = Path(true_top20_file)
+    pred_top60_file = Path(pred_top60_file)
+    token_re = re.compile(r"(Token\s+(\d+):\s*)(\[[^\]]*\])")
     true_t = parse_tokens(true_top20_file, token_re)
     pred_t = parse_tokens(pred_top60_file, token_re)
-    miss = tot = 0
-    for b, heads in true_t.items():
-        for h, toks in heads.items():
-            for t, lst in toks.items():
-                p = set(pred_t.get(b, {}).get(h, {}).get(t, []))
-                miss += sum(1 for x in lst if x not in p)
-                tot += len(lst)
-    return miss / tot if tot else 0.0
+    diff_lines = []
+    block_idx = head_idx = 0
+    with true_top20_file.open() as src:
+        for line in src:
+            m = token_re.search(line)
+            if not m:
+                diff_lines.append(line)
+                continue
+            tid = int(m.group(2))
+            pred = pred_t[block_idx][head_idx][tid]
+            diff = [x for x in true_t[block_idx][head_idx][tid] if x not in pred]
+            diff_lines.append(f"{m.group(1)}{len(diff)}: {diff}\n")
+            if tid == 255 and head_idx == 15:
+                head_idx, block_idx = 0, block_idx + 1
+            elif tid == 255:
+                head_idx += 1
+    out_file = Path("mismatch_idx.txt")
+    out_file.write_text("".join(diff_lines))
+    print(f"Diff file written to: {out_file}")
+    return out_file

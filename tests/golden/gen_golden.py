@@ -244,9 +244,31 @@ def gen_analysis():
         f = os.path.join(d, "idx.txt")
         save_idx_file(idx[:, :, :5, :], f, block_idx=3)
         text = open(f).read()
+    # mismatch_analysis (:159-191): two save_idx_file outputs of a DiT-shaped layer (16 heads
+    # x 256 tokens, so the token-255 / head-15 block stepping runs), indices from a small
+    # alphabet so that both kept and missing entries occur
+    from funcs import mismatch_analysis
+    tk = torch.randint(0, 24, (2, 16, 256, 4), generator=g)  # save_idx_file writes batch entry 1 (:22-29)
+    pk = torch.randint(0, 24, (2, 16, 256, 6), generator=g)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        ft, fp = os.path.join(d, "true.txt"), os.path.join(d, "pred.txt")
+        save_idx_file(tk, ft, block_idx=0)
+        save_idx_file(tk, ft, block_idx=1)  # a second block appended
+        save_idx_file(pk, fp, block_idx=0)
+        save_idx_file(pk, fp, block_idx=1)
+        t_text, p_text = open(ft).read(), open(fp).read()
+        os.chdir(d)
+        try:
+            res = mismatch_analysis(ft, fp)
+            m_text = open(res).read()
+        finally:
+            os.chdir(cwd)
     np.savez_compressed(os.path.join(OUT, "analysis.npz"), idx=idx.numpy(), true_vals=true_vals.numpy(),
                         scores=scores.numpy(), chosen_k=np.float64(total_chosen_k(idx)),
-                        diff=np.float64(diff_idx_analysis(true_vals, scores)), idx_text=np.array(text))
+                        diff=np.float64(diff_idx_analysis(true_vals, scores)), idx_text=np.array(text),
+                        mm_true=np.array(t_text), mm_pred=np.array(p_text), mm_out=np.array(m_text),
+                        mm_name=np.array(str(res)))
     print("wrote analysis")
 
 

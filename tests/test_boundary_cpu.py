@@ -144,3 +144,18 @@ def test_analysis_hooks_vs_reference():
         f = os.path.join(t, "idx.txt")
         A.save_idx_file(idx[:, :, :5, :], f, block_idx=3)
         assert open(f).read() == str(d["idx_text"])
+
+
+def test_mismatch_analysis_vs_reference(tmp_path, monkeypatch):
+    """funcs.mismatch_analysis (analysis.py:159-191) rewrites the true-index file into
+    ./mismatch_idx.txt, token by token; checked against the file the reference wrote
+    for the same two save_idx_file outputs (tests/golden/analysis.npz)."""
+    from mx_quantization_amd.funcs import analysis as A
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "analysis.npz"))
+    ft, fp = tmp_path / "true.txt", tmp_path / "pred.txt"
+    ft.write_text(str(d["mm_true"]))
+    fp.write_text(str(d["mm_pred"]))
+    monkeypatch.chdir(tmp_path)
+    res = A.mismatch_analysis(str(ft), str(fp))
+    assert str(res) == str(d["mm_name"])
+    assert (tmp_path / str(res)).read_text() == str(d["mm_out"])

@@ -541,3 +541,19 @@ def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
                                  pred_mode=mode, elsa_proj=None if proj is None else dev(proj))
     same(host(idx), host(i2), "idx vs unfused op")
     same(host(out), host(o2), "out vs unfused op")
+
+
+def test_analysis_hooks_on_device_tensors(M):
+    """total_chosen_k / diff_idx_analysis (funcs/analysis.py:56-110, :136-157) on device
+    idx / scores -- as the --anal runs call them on the GPU outputs (deit main.py:134-145)
+    -- against the reference's values (analysis.npz)."""
+    from mx_quantization_amd.funcs import analysis as A
+    d = load("analysis.npz")
+    idx = dev(d["idx"])
+    assert A.total_chosen_k(idx) == pytest.approx(float(d["chosen_k"]), rel=1e-12)
+    assert A.diff_idx_analysis(dev(d["true_vals"]), dev(d["scores"])) == pytest.approx(float(d["diff"]), rel=1e-6)
+    # and on the fused op's own device idx: the union coverage of a real top-k output
+    dt = load("attn_deit_tiny.npz")
+    _, gidx = M.mx_topk_attention(dev(dt["q"]), dev(dt["k"]), dev(dt["v"]), float(dt["scale"]), k_top=20)
+    assert A.total_chosen_k(gidx) == pytest.approx(A.total_chosen_k(torch.from_numpy(dt["ex_pred_k20/idx"])),
+                                                   rel=1e-12)
