@@ -223,6 +223,11 @@ int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t it
  * block exponents along in_features into `wq` (mxa_linear_weight_bytes bytes, 16-B
  * aligned; once per weight), laid out MFMA-ready in column groups of group_width
  * (the qkv projection: out_features = 3 * H * D, group_width = D -- one head's q, k or v).
+ * The buffer starts with a header recording out_features, in_features, group_width,
+ * flush_subnormals and bfloat; mxa_qkv_attention returns MXA_ERR_ARG for a buffer whose
+ * header does not match (3*H*D, C, D, p->flush_subnormals, p->bfloat).  A buffer prepared
+ * in another process (or copied) has its header read once, synchronously -- so not
+ * inside a stream capture: call once before capturing.
  *
  * mxa_qkv_attention: mxa_attention with q, k, v produced from x (p->q, p->k, p->v are
  * ignored; self-attention, p->N == p->T).  The projection is exact-then-rounded (the

@@ -244,6 +244,11 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     return MXA_ERR_UNSUPPORTED;
   if (p->bfloat != 0 && p->bfloat != 32 && (p->bfloat < 10 || p->bfloat > 31)) return MXA_ERR_ARG;
   if (p->T > 512 || p->D > 32 * kMaxNB) return MXA_ERR_UNSUPPORTED;
+  // the prepared weight must have been prepared for this geometry and these settings
+  if (xq && !linear_weight_verify(xq->wq, linear_weight_header(3 * p->H * p->D, xq->C, p->D, p->flush_subnormals,
+                                                                p->bfloat),
+                                  stream))
+    return MXA_ERR_ARG;
   mxa_attn_params pp = *p;
   if (scores_only) {  // the selection kernel alone, with no kept keys
     pp.top_k = 0;
@@ -318,6 +323,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   cv.H = pp.H; cv.mats = BH; cv.R = pp.T; cv.C = pp.D; cv.nb = L.ntb; cv.rpad = L.tpad;
   cv.mbits = 8; cv.flush = pp.flush_subnormals; cv.bfloat = pp.bfloat; cv.dt = rq.dt;
   cv.codes_t = reinterpret_cast<int8_t*>(ws + L.vt);
+  cv.tb_major = 1;
   cv.scale = reinterpret_cast<int16_t*>(ws + L.vs);
   if (xq) {
     rc = launch_qkv_proj(pp, *xq, L, rq, rk, cv, ws, stream);

@@ -99,12 +99,12 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
           *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
     }
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tke[i] = a.ksT[kb * nbd + i];
-    const int vpr = a.tpad / 16;
+    // V^T codes, token-block-major in HBM ([ntb][D][32] per head: contiguous 2-KB runs)
     const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
-    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
-      const int d = i / vpr, c = i - d * vpr;
-      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
-          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+    for (int i = threadIdx.x; i < a.ntb * D * 2; i += blockDim.x) {
+      const int half = i & 1, dd = (i >> 1) % D, tb = (i >> 1) / D;
+      *reinterpret_cast<uint4*>(tvt + (size_t)dd * vst + 32 * tb + 16 * half) =
+          *reinterpret_cast<const uint4*>(vsrc + ((int64_t)tb * D + dd) * 32 + 16 * half);
     }
     const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
     for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tve[i] = vssrc[i];
@@ -181,10 +181,9 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
       const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
       const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
       auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
-        bool nan = false;
-        const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
+        const float acc = true_dot<NB>(cur.qv, cur.qe, tkc + (size_t)j * kst, tke + j * nbd);
         // (true scores in the score dtype: the matmul's output, then * scale, + bias)
-        float t = round_bfloat(round_dt(nan ? __uint_as_float(0x7FC00000u) : (float)acc, sdt), a.bfloat, kRoundNearest,
+        float t = round_bfloat(round_dt(acc, sdt), a.bfloat, kRoundNearest,
                               1, sdt);
         t = round_dt(t * a.scale, sdt);
         if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);
@@ -252,10 +251,9 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
         const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
         const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
         auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
-          bool nan = false;
-          const double acc = g_dot<0, NB>(cur.qv, cur.qe, nbd, tkc + (size_t)j * kst, tke + j * nbd, nan);
+          const float acc = true_dot<NB>(cur.qv, cur.qe, tkc + (size_t)j * kst, tke + j * nbd);
           // (true scores in the score dtype: the matmul's output, then * scale, + bias)
-          float t = round_bfloat(round_dt(nan ? __uint_as_float(0x7FC00000u) : (float)acc, sdt), a.bfloat, kRoundNearest,
+          float t = round_bfloat(round_dt(acc, sdt), a.bfloat, kRoundNearest,
                                 1, sdt);
           t = round_dt(t * a.scale, sdt);
           if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);

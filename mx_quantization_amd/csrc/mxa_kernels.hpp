@@ -69,7 +69,9 @@ struct ColsPrepArgs {
   int R, C, nb, rpad;
   int mbits, flush, bfloat;
   int dt;  // storage dtype of x
-  int8_t* codes_t;  // [mats][C][rpad] transposed codes
+  int tb_major;     // codes layout: 0 = [mats][C][rpad]; 1 = [mats][nb][C][32] (the attention's V^T:
+                    // a 32-token block of a head is one contiguous C x 32-byte run, whole lines)
+  int8_t* codes_t;  // transposed codes
   int16_t* scale;   // [mats][nb][C] exponent of a code unit: es - (mbits-2)
 };
 

@@ -16,5 +16,9 @@ int launch_select_p2(const Rows2Args& ra, int mode, int BH, hipStream_t stream, 
 int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan);
 // fused qkv projection kernel (mxa_proj.hip)
 int launch_proj(const ProjArgs& pa, hipStream_t stream);
+// does the prepared weight at wq carry this header?  Buffers prepared in this process
+// are looked up host-side; others have their header read once (not under stream capture)
+LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat);
+bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStream_t stream);
 
 }  // namespace mxa

@@ -154,22 +154,24 @@ __device__ __forceinline__ bool rows_prep_plain(const RowsPrepArgs& a) {
   return (a.bfloat == 0 || a.bfloat == 32) && !a.flush && !a.zind &&
          (a.op_kind == MXA_OP_MXINT8 || (a.op_kind == MXA_OP_SIGN && !a.op));
 }
-template <int EPL>
+// DT >= 0: the storage dtype known at compile time (the fused projection: float32)
+template <int EPL, int DT = -1>
 __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int64_t row, int blk, int sub, int c0,
                                                       const float xv[EPL], bool valid) {
   constexpr int LPB = 32 / EPL;
+  const int dt = DT >= 0 ? DT : a.dt;
   uint32_t mb = 0;
 #pragma unroll
   for (int j = 0; j < EPL; ++j) mb = max(mb, __float_as_uint(xv[j]) & 0x7FFFFFFFu);
   mb = blk_reduce<LPB>(mb, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
   int e_raw;
-  const int es = scale_exponent_dt(mb, 127, a.dt, &e_raw);
+  const int es = scale_exponent_dt(mb, 127, dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   int code[EPL];
   auto quant = [&](auto tiny) {
     const float s = q8_scale(es);
 #pragma unroll
-    for (int j = 0; j < EPL; ++j) code[j] = q8_code<decltype(tiny)::value>(xv[j], s, a.dt);
+    for (int j = 0; j < EPL; ++j) code[j] = q8_code<decltype(tiny)::value>(xv[j], s, dt);
   };
   if (nanblk) {
 #pragma unroll
@@ -207,8 +209,8 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
       // exponent of the MX-quantized block (funcs/exponent_based_prediction.py:35-36):
       // floor(log2(maxc * 2^(es-6))) = floor(log2 maxc) + es - 6 exactly (maxc <= 127)
       int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : 31 - __clz(maxc) + es - 6);
-      if (a.dt != kF32 && !nanblk && maxc != 0)  // log2 rounded to the dtype
-        eA = floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), a.dt)), a.dt);
+      if (dt != kF32 && !nanblk && maxc != 0)  // log2 rounded to the dtype
+        eA = floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), dt)), dt);
       if (a.sT) a.sT[row * a.nb + blk] = exp_to16(nanblk ? kExpNaN : es - 6);
       if (a.sA) a.sA[row * a.nb + blk] = exp_to16(a.op_kind == MXA_OP_SIGN ? eA : (nanblk ? kExpNaN : es - 6));
       if (a.signs) a.signs[row * a.nb + blk] = sw;
@@ -222,23 +224,30 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
 // ---------------------------------------------------------------------------
 // One 32-row block of one column (m = matrix, blk, column c) from its 32 values
 // (already bfloat-rounded, zero beyond the matrix): codes into the transposed
-// [m][C][rpad] table, the exponent into [m][nb][C].
+// [m][C][rpad] table, the exponent into [m][nb][C].  PLAIN: MXINT8, no flush (the
+// caller checked), DT >= 0 the storage dtype known at compile time.
+template <bool PLAIN = false, int DT = -1>
 __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t m, int blk, int c, const float xv[32],
                                                  uint32_t mx) {
   const int r0 = blk * 32;
+  const int dt = DT >= 0 ? DT : a.dt;
   int e_raw;
-  const int es = scale_exponent_dt(mx, 127, a.dt, &e_raw);
+  const int es = scale_exponent_dt(mx, 127, dt, &e_raw);
   const bool nanblk = es == kExpNaN;
-  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  const bool flush = !PLAIN && a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  const int mbits = PLAIN ? 8 : a.mbits;
   uint32_t w[8];
-  if (!flush && !nanblk && a.mbits == 8) {  // the plain MXINT8 case: q8_code
+  if (PLAIN && nanblk) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = 0u;
+  } else if (!flush && !nanblk && mbits == 8) {  // the plain MXINT8 case: q8_code
     const float s = q8_scale(es);
     auto quant = [&](auto tiny) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         int cd[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cd[j] = q8_code<decltype(tiny)::value>(xv[q * 4 + j], s, a.dt);
+        for (int j = 0; j < 4; ++j) cd[j] = q8_code<decltype(tiny)::value>(xv[q * 4 + j], s, dt);
         w[q] = (uint32_t)(cd[0] & 0xFF) | (uint32_t)(cd[1] & 0xFF) << 8 | (uint32_t)(cd[2] & 0xFF) << 16 |
                (uint32_t)cd[3] << 24;
       }
@@ -253,17 +262,17 @@ __device__ __forceinline__ void cols_prep_column(const ColsPrepArgs& a, int64_t 
       for (int j = 0; j < 4; ++j) {
         float v = xv[q * 4 + j];
         if (flush) v = v * 0.0f;
-        const int cd = nanblk ? 0 : (int)round_code(v, es, a.mbits, kRoundNearest, a.dt);
+        const int cd = nanblk ? 0 : (int)round_code(v, es, mbits, kRoundNearest, dt);
         acc |= (uint32_t)(cd & 0xFF) << (8 * j);
       }
       w[q] = acc;
     }
   }
-  int8_t* dst = a.codes_t + (m * a.C + c) * a.rpad + r0;
+  int8_t* dst = a.tb_major ? a.codes_t + ((m * a.nb + blk) * a.C + c) * 32 : a.codes_t + (m * a.C + c) * a.rpad + r0;
   uint4* d4 = reinterpret_cast<uint4*>(dst);
   d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
   d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  a.scale[(m * a.nb + blk) * a.C + c] = exp_to16(nanblk ? kExpNaN : es - (a.mbits - 2));
+  a.scale[(m * a.nb + blk) * a.C + c] = exp_to16(nanblk ? kExpNaN : es - (mbits - 2));
 }
 
 

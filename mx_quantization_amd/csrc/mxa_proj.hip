@@ -2,6 +2,7 @@
 // entry points of include/mxa.h.
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <utility>
 
 #include "mxa_launch.hpp"
@@ -55,11 +56,23 @@ __global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, in
 }
 
 // ---- fused qkv projection (mxa_proj.hpp) ------------------------------------------
-template <int NBD>
+// the operands' settings leave only the plain rounding (qkv_proj_kernel<NBD, true>)
+static bool proj_plain(const ProjArgs& pa) {
+  auto plain_bf = [](int bf) { return bf == 0 || bf == 32; };
+  auto plain_rows = [&](const RowsPrepArgs& r) {
+    return plain_bf(r.bfloat) && !r.flush && !r.zind && r.dt == kF32 &&
+           (r.op_kind == MXA_OP_MXINT8 || (r.op_kind == MXA_OP_SIGN && !r.op));
+  };
+  return plain_bf(pa.bfloat) && pa.autocast == 0 && plain_rows(pa.rq) && plain_rows(pa.rk) && pa.cv.mbits == 8 &&
+         !pa.cv.flush && plain_bf(pa.cv.bfloat) && pa.cv.dt == kF32;
+}
+
+template <int NBD, bool PLAIN>
 static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   const size_t lds = proj_lds(pa.Cpad, pa.nbk, pa.D).total;
   if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
+  const void* kern = reinterpret_cast<const void*>(&qkv_proj_kernel<NBD, PLAIN>);
+  if (hipFuncSetAttribute(kern,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   // head groups: a workgroup loops over hpg heads after staging its x tile once; the
@@ -72,14 +85,12 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   int per_cu = 1, cus = 256;
   {
     static std::mutex mu;
-    static std::map<std::pair<int, size_t>, std::pair<int, int>> cache;
+    static std::map<std::pair<int, size_t>, std::pair<int, int>> cache;  // per instantiation
     std::lock_guard<std::mutex> lock(mu);
     auto it = cache.find({dev, lds});
     if (it == cache.end()) {
       int n = 0, c = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&qkv_proj_kernel<NBD>),
-                                                       64 * 3 * NBD, lds) != hipSuccess || n < 1)
-        n = 1;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 64 * 3 * NBD, lds) != hipSuccess || n < 1) n = 1;
       if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
       it = cache.emplace(std::make_pair(dev, lds), std::make_pair(n, c)).first;
     }
@@ -101,19 +112,61 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   }
   p.hpg = (pa.H + best_g - 1) / best_g;
   const int ng = (pa.H + p.hpg - 1) / p.hpg;
-  hipLaunchKernelGGL(qkv_proj_kernel<NBD>, dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
+  hipLaunchKernelGGL((qkv_proj_kernel<NBD, PLAIN>), dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
                      dim3(64 * 3 * NBD), lds, stream, p);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
 
-int launch_proj(const ProjArgs& pa, hipStream_t stream) {
+template <bool PLAIN>
+static int launch_proj_p(const ProjArgs& pa, hipStream_t stream) {
   switch ((pa.D + 31) / 32) {
-    case 1: return launch_proj_nbd<1>(pa, stream);
-    case 2: return launch_proj_nbd<2>(pa, stream);
-    case 3: return launch_proj_nbd<3>(pa, stream);
-    default: return launch_proj_nbd<4>(pa, stream);
+    case 1: return launch_proj_nbd<1, PLAIN>(pa, stream);
+    case 2: return launch_proj_nbd<2, PLAIN>(pa, stream);
+    case 3: return launch_proj_nbd<3, PLAIN>(pa, stream);
+    default: return launch_proj_nbd<4, PLAIN>(pa, stream);
   }
+}
+
+int launch_proj(const ProjArgs& pa, hipStream_t stream) {
+  return proj_plain(pa) ? launch_proj_p<true>(pa, stream) : launch_proj_p<false>(pa, stream);
+}
+
+__global__ void linear_header_kernel(LinearWeightHeader* h, LinearWeightHeader v) {
+  if (threadIdx.x == 0) *h = v;
+}
+
+// prepared buffers whose header is known to the host (pointer -> header)
+static std::mutex g_wmu;
+static std::unordered_map<const void*, LinearWeightHeader> g_weights;
+
+static void linear_weight_note(const void* wq, const LinearWeightHeader& h) {
+  std::lock_guard<std::mutex> g(g_wmu);
+  g_weights[wq] = h;
+}
+
+bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStream_t stream) {
+  {
+    std::lock_guard<std::mutex> g(g_wmu);
+    auto it = g_weights.find(wq);
+    if (it != g_weights.end()) return it->second == want;
+  }
+  // a buffer prepared elsewhere (another process, or copied): read its header once
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  LinearWeightHeader h{};
+  if (hipMemcpyAsync(&h, wq, sizeof(h), hipMemcpyDeviceToHost, stream) != hipSuccess) return false;
+  if (hipStreamSynchronize(stream) != hipSuccess) return false;
+  if (!(h == want)) return false;
+  linear_weight_note(wq, h);
+  return true;
+}
+
+LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat) {
+  LinearWeightHeader h{};
+  h.magic = kLinearWeightMagic; h.version = 1;
+  h.out_f = out_f; h.in_f = in_f; h.gw = gw; h.flush = flush ? 1 : 0; h.bfloat = bfloat;
+  return h;
 }
 
 }  // namespace mxa
@@ -149,6 +202,11 @@ extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int3
   if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   hipLaunchKernelGGL(linear_stats_kernel, dim3((unsigned)((pcols + 255) / 256)), dim3(256), 0, stream,
                      reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps));
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+  const LinearWeightHeader h = linear_weight_header(out_features, in_features, group_width, flush_subnormals, bfloat);
+  hipLaunchKernelGGL(linear_header_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<LinearWeightHeader*>(wb + W.hdr),
+                     h);
+  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  linear_weight_note(wq, h);
+  return MXA_OK;
 }
 

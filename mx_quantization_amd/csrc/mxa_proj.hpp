@@ -10,8 +10,10 @@
 // MX block, so each block's int32 sum is exact -- with the block scale 2^(ex + ew)
 // applied exactly -- as int32 sums shifted to the row's and column's smallest block
 // exponent (the common case; v_lshl_add_u32), else in fp64 -- so the projection is
-// the correctly rounded exact product (the reference's MKL sgemm order is unpinned, SURVEY.md F7:
-// tolerance there, bit-exact against the oracle).  The fp32 tile then stays in LDS
+// the correctly rounded exact product whenever the blocks' scaled exponents span <= 34
+// bits (fp64 holds such a sum exactly); wider spreads round in the fp64 sum and again
+// to fp32, i.e. within fp32 rounding (the reference's MKL sgemm order is unpinned,
+// tolerance there, bit-exact against the oracle on the tested spreads).  The fp32 tile then stays in LDS
 // and is quantized in place into exactly what rows_prep / cols_prep would produce
 // from q, k, v: q and k rows (codes, block exponents, approximator operands) and V's
 // codes along the 32 tokens (transposed) -- the fp32 q / k / v never reach HBM.
@@ -32,8 +34,10 @@ struct ProjLds {
 };
 // x code tile [32][Cpad + 16], x exponents relative to the row's smallest [nbk][32]
 // (int16, NaN -> 0), per-row smallest / largest exponent and NaN flag, tile stats, the
-// fp32 output tile of one head [32][3D + 1] (odd stride: V's column reads are
-// conflict-free)
+// fp32 output tile of one head [32][96 NBD + 1]: q, k, v at columns 0, 32 NBD, 64 NBD
+// (padding columns beyond D take the padded MFMA columns, so every lane stores
+// unpredicated; the odd stride keeps V's column reads conflict-free; compile-time, so
+// the epilogue's 16 stores take immediate offsets)
 __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   ProjLds L;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -51,7 +55,7 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   o += 32 * 4;
   L.st = o;
   o += 16;
-  L.ost = 3 * D + 1;
+  L.ost = 96 * ((D + 31) / 32) + 1;
   L.ot = o;
   o += al((size_t)32 * L.ost * 4);
   L.total = o;
@@ -66,10 +70,14 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #ifndef MXA_PROJ_PF
 #define MXA_PROJ_PF 2  // K-blocks of weight codes in flight per wave (measured: 4 and 8 slower, registers)
 #endif
-template <int NBD>
+// PLAIN (proj_plain): no bfloat rounding, no flush, no autocast, q / k operands of
+// rows_prep_block_plain and V's MXINT8 -- the bench path, compiled without the general
+// rounding code (a third of the code and registers of the general instantiation)
+template <int NBD, bool PLAIN>
 __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int kThreads = 64 * 3 * NBD;
+  constexpr int kOst = 96 * NBD + 1;  // == proj_lds(...).ost
   const int tb = blockIdx.x, b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int D = a.D, HD = a.H * D, nbk = a.nbk;
@@ -152,60 +160,59 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
     // row and column exponent spreads sum to <= smax, the block sums shifted by
     // (ex - rowmin) + (ew - colmin) add up exactly in int32, and one conversion gives
     // the correctly rounded result (2 VALU per element and block).  Otherwise (or when
-    // the result could be subnormal) each block is added exactly in fp64.
+    // the result could be subnormal) the blocks are summed in fp64: exact while their
+    // scaled exponents span <= 34 bits, within fp32 rounding beyond that.
     const int wsp_max = (int)wave_max_u32((uint32_t)wsp);
     const int wlo_min =
         (int)wave_reduce((uint32_t)(wlo + (1 << 20)), [](uint32_t u, uint32_t w) { return u < w ? u : w; }) - (1 << 20);
     const bool fast = st[0] + wsp_max <= a.smax && st[1] + wlo_min >= -126;
     const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
-    const float bb = (a.bias && colv) ? round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1) : 0.0f;
+    const float bb = (a.bias && colv) ? (PLAIN ? a.bias[jcol] : round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1)) : 0.0f;
     // the K loop and the epilogue, specialised on the accumulation (FAST: shifted int32;
-    // else exact fp64): separate live ranges, so the two never hold registers together
+    // else fp64): separate live ranges, so the two never hold registers together
     auto run = [&](auto fast_c) {
       constexpr bool FAST = decltype(fast_c)::value;
       typename std::conditional<FAST, int, double>::type acc[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0;
-      // the weight codes and the column's block exponents ride kPf K-blocks ahead (a
-      // load per block issued right before its use left an L2 round trip on every
-      // step), the x operand one block ahead
-      constexpr int kPf = MXA_PROJ_PF;
-      v4i_ bq[kPf];
-      int16_t eq[kPf];
-#pragma unroll
-      for (int i = 0; i < kPf; ++i) {
-        const int kk = i < nbk ? i : 0;
-        bq[i] = *reinterpret_cast<const v4i_*>(wp + kk * 1024);
-        eq[i] = wep[kk];
-      }
-      v4i_ an = *reinterpret_cast<const v4i_*>(xa);
-      for (int kb = 0; kb < nbk; ++kb) {
-        const v4i_ bv = bq[0];
-        const int16_t ewr = eq[0];
-#pragma unroll
-        for (int i = 0; i + 1 < kPf; ++i) {
-          bq[i] = bq[i + 1];
-          eq[i] = eq[i + 1];
-        }
-        if (kb + kPf < nbk) {
-          bq[kPf - 1] = *reinterpret_cast<const v4i_*>(wp + (kb + kPf) * 1024);
-          eq[kPf - 1] = wep[kb + kPf];
-        }
-        const v4i_ av = an;
-        if (kb + 1 < nbk) an = *reinterpret_cast<const v4i_*>(xa + 32 * (kb + 1));
-        const v16i zero = {};
-        const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
-        int ew = exp_from16(ewr);
-        cnan = cnan || ew == kExpNaN;
-        ew = ew == kExpNaN ? wlo : ew;
+      // Software pipeline over the K-blocks: the MFMA of block kb + 1 is issued before the
+      // epilogue of block kb, so the matrix core works while the VALU shifts and adds;
+      // the operands (weight codes: one coalesced 1-KB load per wave, x codes from the
+      // LDS tile, the column's block exponent) and the rows' exponent offsets ride one
+      // block further ahead.
+      auto ldw = [&](int kb) { return *reinterpret_cast<const v4i_*>(wp + kb * 1024); };
+      auto ldx = [&](int kb) { return *reinterpret_cast<const v4i_*>(xa + 32 * kb); };
+      auto lde = [&](int kb, uint2 (&e)[4]) {
         const int16_t* eb = xe + kb * 32 + m0;
 #pragma unroll
+        for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2*>(eb + 8 * q);  // rows 8q + m0 .. + 3
+      };
+      const v16i zero = {};
+      v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ldx(0), ldw(0), zero, 0, 0, 0);
+      int16_t ecur = wep[0];
+      uint2 xcur[4];
+      lde(0, xcur);
+      const int k1 = nbk > 1 ? 1 : 0;
+      v4i_ an = ldx(k1), bn = ldw(k1);
+      int16_t en = wep[k1];
+      uint2 xn[4];
+      lde(k1, xn);
+      for (int kb = 0; kb < nbk; ++kb) {
+        const int k2 = kb + 2 < nbk ? kb + 2 : nbk - 1;
+        const v4i_ a2 = ldx(k2), b2 = ldw(k2);
+        const int16_t e2 = wep[k2];
+        const v16i cn = kb + 1 < nbk ? __builtin_amdgcn_mfma_i32_32x32x32_i8(an, bn, zero, 0, 0, 0) : c;
+        int ew = exp_from16(ecur);
+        cnan = cnan || ew == kExpNaN;
+        ew = ew == kExpNaN ? wlo : ew;
+        const int ewd = ew - wlo;
+#pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint2 e4 = *reinterpret_cast<const uint2*>(eb + 8 * q);  // rows 8q + m0 .. + 3
+          const uint2 e4 = xcur[q];
           const int dx[4] = {(int)(e4.x & 0xFFFFu), (int)(e4.x >> 16), (int)(e4.y & 0xFFFFu), (int)(e4.y >> 16)};
           if constexpr (FAST) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[4 * q + r] += (int)((uint32_t)c[4 * q + r] << (dx[r] + ew - wlo));
+            for (int r = 0; r < 4; ++r) acc[4 * q + r] += (int)((uint32_t)c[4 * q + r] << (dx[r] + ewd));
           } else {
             const int4 lo4 = *reinterpret_cast<const int4*>(rlo + 8 * q + m0);
             const int lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
@@ -213,27 +220,52 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
             for (int r = 0; r < 4; ++r) acc[4 * q + r] += ldexp((double)c[4 * q + r], dx[r] + lo[r] + ew);
           }
         }
+        c = cn;
+        ecur = en;
+        en = e2;
+        an = a2;
+        bn = b2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xcur[q] = xn[q];
+        lde(k2, xn);
       }
       // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -------
+      // branch-free: NaN by select; bb = 0 without a bias and o + 0 = o here (o is never
+      // -0: an int32 sum converts to +0)
+      float* orow = ot + m0 * kOst + s * 32 * NBD + dcol;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = 8 * (i >> 2) + m0 + (i & 3);
-        float o;
-        if constexpr (FAST) o = ldexpf((float)acc[i], rlo[m] + wlo);
-        else o = (float)acc[i];
-        if (cnan || rn[m]) o = __uint_as_float(0x7FC00000u);
-        o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
-        o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
-        if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
-        if (colv) {
-          ot[m * L.ost + s * D + dcol] = o;
-          if (a.qkv_out && m < rows) a.qkv_out[(row0 + m) * (3 * HD) + jcol] = o;
+      for (int q = 0; q < 4; ++q) {
+        const int4 lo4 = *reinterpret_cast<const int4*>(rlo + 8 * q + m0);
+        const int4 rn4 = *reinterpret_cast<const int4*>(rn + 8 * q + m0);
+        const int lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w}, nf[4] = {rn4.x, rn4.y, rn4.z, rn4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o;
+          if constexpr (FAST) o = ldexpf((float)acc[4 * q + r], lo[r] + wlo);
+          else o = (float)acc[4 * q + r];
+          o = (cnan || nf[r]) ? __uint_as_float(0x7FC00000u) : o;
+          if constexpr (PLAIN) {
+            o += bb;
+          } else {
+            o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+            o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
+            if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
+          }
+          orow[(8 * q + r) * kOst] = o;
         }
       }
     };
     if (fast) run(std::integral_constant<bool, true>{});
     else run(std::integral_constant<bool, false>{});
     __syncthreads();
+    if (a.qkv_out) {  // the fp32 projection (tests): whole rows of the tile, coalesced
+      for (int i = threadIdx.x; i < 32 * 3 * D; i += kThreads) {
+        const int m = i / (3 * D), col = i - m * (3 * D), sc = col / D;
+        if (m < rows)
+          a.qkv_out[(row0 + m) * (3 * HD) + (int64_t)sc * HD + (int64_t)h * D + (col - sc * D)] =
+              ot[m * kOst + sc * 32 * NBD + col - sc * D];
+      }
+    }
 
     // ---- q and k rows (waves 0 .. 2 NBD - 1) beside V's columns (the other NBD waves:
     // 64 NBD >= D lanes, one column each).  Before, the wave that took the first q rows
@@ -251,22 +283,27 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
       const int c0 = 32 * blk + 16 * sub;
       float xv[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) xv[j] = c0 + j < D ? ot[m * L.ost + sk * D + c0 + j] : 0.0f;
+      for (int j = 0; j < 16; ++j) xv[j] = c0 + j < D ? ot[m * kOst + sk * 32 * NBD + c0 + j] : 0.0f;
       const RowsPrepArgs& ra = sk ? a.rk : a.rq;
-      if (rows_prep_plain(ra)) rows_prep_block_plain<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
-      else rows_prep_block<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+      if constexpr (PLAIN) {
+        rows_prep_block_plain<16, kF32>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+      } else {
+        if (rows_prep_plain(ra)) rows_prep_block_plain<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+        else rows_prep_block<16>(ra, hrow0 + m, blk, sub, c0, xv, m < rows);
+      }
     } else if (const int c = (int)threadIdx.x - 2 * kPer; c < D) {
       // V: cols_prep's per-column body over the 32 tokens
       float xv[32];
       uint32_t mx = 0;
 #pragma unroll
       for (int j = 0; j < 32; ++j) {
-        const float v = j < rows ? round_bfloat(ot[j * L.ost + 2 * D + c], a.cv.bfloat, kRoundNearest, 1) : 0.0f;
+        const float v = j >= rows ? 0.0f : PLAIN ? ot[j * kOst + 64 * NBD + c]
+                                                 : round_bfloat(ot[j * kOst + 64 * NBD + c], a.cv.bfloat, kRoundNearest, 1);
         xv[j] = v;
         const uint32_t ub = __float_as_uint(v) & 0x7FFFFFFFu;
         mx = ub > mx ? ub : mx;
       }
-      cols_prep_column(a.cv, hrow_b + h, tb, c, xv, mx);
+      cols_prep_column<PLAIN, PLAIN ? kF32 : -1>(a.cv, hrow_b + h, tb, c, xv, mx);
     }
     __syncthreads();
   }

@@ -11,9 +11,21 @@ namespace mxa {
 //   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
 //   ps  per padded column: smallest finite block exponent, spread (int16 pair)
 //   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
+//   hdr the geometry and settings it was prepared with (LinearWeightHeader, 256 B at
+//       offset 0, so a buffer of any size holds it): mxa_qkv_attention refuses a buffer
+//       whose header does not match the call instead of reading past its end
 struct LinearLayout {
   int G, NB32, nbk, Cpad;
-  int64_t pk, pe, ps, rawc, rawe, total;
+  int64_t hdr, pk, pe, ps, rawc, rawe, total;
+};
+constexpr uint32_t kLinearWeightMagic = 0x5741584du;  // "MXAW"
+struct LinearWeightHeader {
+  uint32_t magic;
+  int32_t version, out_f, in_f, gw, flush, bfloat, reserved;
+  bool operator==(const LinearWeightHeader& o) const {
+    return magic == o.magic && version == o.version && out_f == o.out_f && in_f == o.in_f && gw == o.gw &&
+           flush == o.flush && bfloat == o.bfloat;
+  }
 };
 __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int gw) {
   LinearLayout L;
@@ -24,6 +36,8 @@ __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int g
   L.Cpad = 32 * L.nbk;
   const int64_t pcols = (int64_t)L.G * L.NB32 * 32;
   int64_t o = 0;
+  L.hdr = o;
+  o += 256;
   L.pk = o;
   o += al(pcols * L.Cpad);
   L.pe = o;

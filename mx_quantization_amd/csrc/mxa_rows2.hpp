@@ -133,12 +133,12 @@ __global__ __launch_bounds__(1024, 1) void dense_rows_kernel(Rows2Args a) {
           *reinterpret_cast<const uint4*>(a.kc + (kb + j) * a.dpad + 16 * c);
     }
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tsT[i] = a.ksT[kb * nbd + i];
-    const int vpr = a.tpad / 16;
+    // V^T codes, token-block-major in HBM ([ntb][D][32] per head: contiguous 2-KB runs)
     const int8_t* vsrc = a.vt + (int64_t)bh * D * a.tpad;
-    for (int i = threadIdx.x; i < D * vpr; i += blockDim.x) {
-      const int d = i / vpr, c = i - d * vpr;
-      *reinterpret_cast<uint4*>(tvt + (size_t)d * vst + 16 * c) =
-          *reinterpret_cast<const uint4*>(vsrc + (int64_t)d * a.tpad + 16 * c);
+    for (int i = threadIdx.x; i < a.ntb * D * 2; i += blockDim.x) {
+      const int half = i & 1, dd = (i >> 1) % D, tb = (i >> 1) / D;
+      *reinterpret_cast<uint4*>(tvt + (size_t)dd * vst + 32 * tb + 16 * half) =
+          *reinterpret_cast<const uint4*>(vsrc + ((int64_t)tb * D + dd) * 32 + 16 * half);
     }
     const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
     for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = vssrc[i];

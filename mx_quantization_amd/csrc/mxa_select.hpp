@@ -134,6 +134,41 @@ __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd,
   return acc;
 }
 
+// The true score fl32(sum_b I_b 2^(qe_b + ke_b)) of a query row (codes in registers)
+// and a key row of the LDS code table (MXINT8, exponents in code units): block sums by
+// v_dot4; when the block exponents span <= 10 bits (NB x 2^19 x 2^10 < 2^31) and the
+// smallest is >= -100, the sum shifted to the smallest exponent is an exact int32 and
+// one conversion + exact scaling gives the correctly rounded float (no fp64); otherwise
+// the exact fp64 sum (g_dot).  NaN for a NaN block.
+template <int NB>
+__device__ __forceinline__ float true_dot(const uint4* qv, const int* qe, const int8_t* krow, const int16_t* kexp) {
+  int I[NB], e[NB];
+  int emin = 1 << 20, emax = -(1 << 20);
+  bool nan = false;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
+    const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
+    I[b] = dot32(qv[2 * b], qv[2 * b + 1], x0, x1);
+    const int ke = exp_from16(kexp[b]);
+    nan = nan || ke == kExpNaN || qe[b] == kExpNaN;
+    e[b] = qe[b] + ke;
+    emin = min(emin, e[b]);
+    emax = max(emax, e[b]);
+  }
+  if (nan) return __uint_as_float(0x7FC00000u);
+  if (emax - emin <= 10 && emin >= -100) {
+    int sum = 0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sum += I[b] << (e[b] - emin);
+    return ldexpf((float)sum, emin);
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc += (double)I[b] * pow2d(e[b]);
+  return (float)acc;
+}
+
 // true_ex: a = c * 2^e + z per element (c the power-of-two code, 0 for a zero MX
 // element; z = 1 for a zero element), so per block
 //   sum aQ aK = 2^(eq+ek) <cq,ck> + 2^eq <cq,zk> + 2^ek <zq,ck> + <zq,zk>   (exact in fp64)

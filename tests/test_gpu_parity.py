@@ -504,10 +504,12 @@ def test_qkv_attention_vs_reference(M):
 
 
 @pytest.mark.parametrize("mode", ["ex_pred", "MXINT4", "two_step_leading_ones", "true_ex", "partial_Q", "ELSA"])
-@pytest.mark.parametrize("B,N,C,H", [(2, 197, 768, 12), (1, 256, 1152, 16), (3, 45, 96, 2)])
-def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
+@pytest.mark.parametrize("B,N,C,H,k_top", [(2, 197, 768, 12, 20), (2, 197, 768, 12, 30), (1, 256, 1152, 16, 154),
+                                           (3, 45, 96, 2, 20)])
+def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H, k_top):
     """The fused projection + attention against the oracle chained the same way (exact
-    projection, split, attention) at the DeiT-base and DiT-XL/2 block widths and a
+    projection, split, attention) on every image, at the DeiT-base (k = 20 and the
+    --topk 30 variant) and DiT-XL/2 (k = 154, the 0.6 x 256 of the bench) block widths and a
     ragged small case; NaN token row and zero weight row included."""
     D = C // H
     if mode == "ELSA" and D not in (64, 72):
@@ -518,7 +520,7 @@ def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
     bias = (rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
     x[0, 3, 7] = np.nan
     W[5] = 0.0
-    k = min(20, N)
+    k = min(k_top, N)
     proj = None
     if mode == "ELSA":
         from mx_quantization_amd.funcs import _create_structured_orthogonal_matrix
@@ -532,15 +534,41 @@ def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H):
     same(host(qkv), want_qkv, "qkv")
     # the operands the fused kernel produced equal those of the unfused op on its q, k, v
     q, kk, v = O.qkv_split(want_qkv, H)
-    sub = slice(0, 1)  # oracle on the first image (all images through the unfused op)
-    r = O.attention(q[sub], kk[sub], v[sub], D ** -0.5, k_top=k, pred_mode=mode, elsa_proj=proj)
-    same(host(idx)[sub], r["idx"], "idx vs oracle")
+    r = O.attention(q, kk, v, D ** -0.5, k_top=k, pred_mode=mode, elsa_proj=proj)
+    same(host(idx), r["idx"], "idx vs oracle")
     o_fin = ~np.isnan(r["out"]).any(-1)
-    assert O.normwise_rel_err(host(out)[sub][o_fin], r["out"][o_fin]) <= OUT_TOL
+    assert O.normwise_rel_err(host(out)[o_fin], r["out"][o_fin]) <= OUT_TOL
     o2, i2 = M.mx_topk_attention(*(dev(np.ascontiguousarray(t)) for t in (q, kk, v)), D ** -0.5, k_top=k,
                                  pred_mode=mode, elsa_proj=None if proj is None else dev(proj))
     same(host(idx), host(i2), "idx vs unfused op")
     same(host(out), host(o2), "out vs unfused op")
+
+
+def test_qkv_weight_header_checked(M):
+    """mxa_qkv_attention refuses a prepared weight whose header does not match the call
+    (ADVICE r2): other settings, an unprepared buffer; a copy of a good one is accepted
+    (its header is read once) and gives the same result."""
+    rng = np.random.default_rng(7)
+    x = dev(rng.standard_normal((1, 64, 128), dtype=np.float32))
+    W = dev(rng.standard_normal((3 * 128, 128), dtype=np.float32) * np.float32(0.05))
+    wq = M.LinearWeightMX(W, 64)
+    o1, i1 = M.mx_qkv_attention(x, wq, None, 2, 0.125, k_top=10)
+    cp = M.LinearWeightMX.__new__(M.LinearWeightMX)
+    cp.__dict__.update(wq.__dict__)
+    cp.buf = wq.buf.clone()
+    o2, i2 = M.mx_qkv_attention(x, cp, None, 2, 0.125, k_top=10)
+    same(host(i1), host(i2), "copied weight idx")
+    same(host(o1), host(o2), "copied weight out")
+    spoof = M.LinearWeightMX.__new__(M.LinearWeightMX)
+    spoof.__dict__.update(wq.__dict__)
+    spoof.bfloat = 16  # passes the Python check, the header says bfloat 0
+    with pytest.raises(M.NativeError):
+        M.mx_qkv_attention(x, spoof, None, 2, 0.125, k_top=10, bfloat=16)
+    blank = M.LinearWeightMX.__new__(M.LinearWeightMX)
+    blank.__dict__.update(wq.__dict__)
+    blank.buf = torch.zeros_like(wq.buf)
+    with pytest.raises(M.NativeError):
+        M.mx_qkv_attention(x, blank, None, 2, 0.125, k_top=10)
 
 
 def test_analysis_hooks_on_device_tensors(M):
