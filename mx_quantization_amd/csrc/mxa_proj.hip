@@ -1,5 +1,6 @@
 // The fused qkv projection's launches (mxa_proj.hpp) and the Linear weight preparation
 // entry points of include/mxa.h.
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -53,6 +54,20 @@ __global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, in
   if (lo > hi) lo = hi = 0;
   ps[2 * pc] = (int16_t)lo;
   ps[2 * pc + 1] = (int16_t)(hi - lo);
+}
+
+// per group of gw real columns: smallest column exponent, largest column spread
+__global__ __launch_bounds__(64) void linear_group_stats_kernel(const int16_t* ps, int G, int NB32, int gw, int16_t* gs) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  int lo = 1 << 20, sp = 0;
+  for (int gc = 0; gc < gw; ++gc) {
+    const int64_t pc = ((int64_t)g * NB32 + gc / 32) * 32 + gc % 32;
+    lo = min(lo, (int)ps[2 * pc]);
+    sp = max(sp, (int)ps[2 * pc + 1]);
+  }
+  gs[2 * g] = (int16_t)lo;
+  gs[2 * g + 1] = (int16_t)sp;
 }
 
 // ---- fused qkv projection (mxa_proj.hpp) ------------------------------------------
@@ -114,6 +129,15 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   const int ng = (pa.H + p.hpg - 1) / p.hpg;
   hipLaunchKernelGGL((qkv_proj_kernel<NBD, PLAIN>), dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
                      dim3(64 * 3 * NBD), lds, stream, p);
+  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  // the heads listed for the fp64 block sums (usually none: every workgroup reads the
+  // count and leaves)
+  const void* slow = reinterpret_cast<const void*>(&qkv_proj_slow_kernel<NBD, PLAIN>);
+  if (hipFuncSetAttribute(slow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const int64_t entries = (int64_t)pa.ntb * pa.B * pa.H;
+  const unsigned sgrid = (unsigned)std::min<int64_t>(entries, (int64_t)cus);
+  hipLaunchKernelGGL((qkv_proj_slow_kernel<NBD, PLAIN>), dim3(sgrid), dim3(64 * 3 * NBD), lds, stream, p);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 
@@ -164,7 +188,7 @@ bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStr
 
 LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat) {
   LinearWeightHeader h{};
-  h.magic = kLinearWeightMagic; h.version = 1;
+  h.magic = kLinearWeightMagic; h.version = 2;
   h.out_f = out_f; h.in_f = in_f; h.gw = gw; h.flush = flush ? 1 : 0; h.bfloat = bfloat;
   return h;
 }
@@ -202,6 +226,9 @@ extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int3
   if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   hipLaunchKernelGGL(linear_stats_kernel, dim3((unsigned)((pcols + 255) / 256)), dim3(256), 0, stream,
                      reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps));
+  hipLaunchKernelGGL(linear_group_stats_kernel, dim3((unsigned)((W.G + 63) / 64)), dim3(64), 0, stream,
+                     reinterpret_cast<const int16_t*>(wb + W.ps), W.G, W.NB32, group_width,
+                     reinterpret_cast<int16_t*>(wb + W.gs));
   const LinearWeightHeader h = linear_weight_header(out_features, in_features, group_width, flush_subnormals, bfloat);
   hipLaunchKernelGGL(linear_header_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<LinearWeightHeader*>(wb + W.hdr),
                      h);

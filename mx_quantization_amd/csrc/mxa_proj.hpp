@@ -67,18 +67,17 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #ifndef MXA_PROJ_WAVES
 #define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
 #endif
-#ifndef MXA_PROJ_PF
-#define MXA_PROJ_PF 2  // K-blocks of weight codes in flight per wave (measured: 4 and 8 slower, registers)
-#endif
 // PLAIN (proj_plain): no bfloat rounding, no flush, no autocast, q / k operands of
 // rows_prep_block_plain and V's MXINT8 -- the bench path, compiled without the general
-// rounding code (a third of the code and registers of the general instantiation)
-template <int NBD, bool PLAIN>
-__global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// rounding code (a third of the code and registers of the general instantiation).
+// SLOW: the block sums in fp64 (qkv_proj_slow_kernel); else in shifted int32, and a head
+// whose exponent spreads do not allow that is listed for the slow kernel -- so the
+// common kernel carries no fp64 code and no registers for it.
+template <int NBD, bool PLAIN, bool SLOW>
+__device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int h_begin, int h_end,
+                                           unsigned char* smem) {
   constexpr int kThreads = 64 * 3 * NBD;
   constexpr int kOst = 96 * NBD + 1;  // == proj_lds(...).ost
-  const int tb = blockIdx.x, b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int D = a.D, HD = a.H * D, nbk = a.nbk;
   const ProjLds L = proj_lds(a.Cpad, nbk, D);
@@ -140,32 +139,49 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
   // lane maps of v_mfma_i32_32x32x32_i8 (mxa_selftest_mfma32): A[m][k], m = lane % 32,
   // k = 16 (lane / 32) + 0..15; B[k][n], n = lane % 32; C[m][n] in c[i],
   // m = 8 (i / 4) + 4 (lane / 32) + i % 4
-  const int s = wave / NBD, cb = wave - s * NBD;
+  // uniform per wave (readfirstlane: the weight addresses then live in SGPRs, the
+  // per-lane part is a loop-invariant VGPR offset)
+  const int s = __builtin_amdgcn_readfirstlane(wave / NBD), cb = __builtin_amdgcn_readfirstlane(wave - s * NBD);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.pk), 0, a.pk_bytes, 0x00020000);
+  const auto ers = __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(a.pe), 0, a.pe_bytes, 0x00020000);
   const int ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
   const int dcol = 32 * cb + ln;
   const bool colv = dcol < D;
   const int8_t* xa = xt + ln * L.xst + kh;
   const int64_t hrow_b = (int64_t)b * a.H;
 
-  const int h_end = min(a.H, ((int)blockIdx.z + 1) * a.hpg);
-  for (int h = (int)blockIdx.z * a.hpg; h < h_end; ++h) {
+  for (int h = h_begin; h < h_end; ++h) {
     // ---- this wave's 32 x 32 output block of head h -------------------------------
     const int64_t blkc = (int64_t)(s * a.H + h) * NBD + cb;  // padded 32-column block
     const int64_t pc = 32 * blkc + ln;
-    const int8_t* wp = a.pk + (blkc * nbk) * 1024 + lane * 16;
-    const int16_t* wep = a.pe + pc * nbk;
-    const int wlo = a.ps[2 * pc], wsp = a.ps[2 * pc + 1];
+    // buffer loads: descriptor and the K-block's offset in SGPRs, the per-lane part a
+    // loop-invariant VGPR (no per-load address arithmetic; checked by proj_buffers_fit)
+    const int wsoff = __builtin_amdgcn_readfirstlane((int)(blkc * nbk) * 1024);
+    const int esoff = __builtin_amdgcn_readfirstlane((int)(32 * blkc * nbk) * 2);
+    const int woff = lane * 16, eoff = ln * nbk * 2;
+    const int wlo = a.ps[2 * pc];
     bool cnan = false;
     // Every block product is c * 2^(ex + ew) with |c| <= 32 * 127^2 < 2^19.  When the
     // row and column exponent spreads sum to <= smax, the block sums shifted by
     // (ex - rowmin) + (ew - colmin) add up exactly in int32, and one conversion gives
     // the correctly rounded result (2 VALU per element and block).  Otherwise (or when
-    // the result could be subnormal) the blocks are summed in fp64: exact while their
-    // scaled exponents span <= 34 bits, within fp32 rounding beyond that.
-    const int wsp_max = (int)wave_max_u32((uint32_t)wsp);
-    const int wlo_min =
-        (int)wave_reduce((uint32_t)(wlo + (1 << 20)), [](uint32_t u, uint32_t w) { return u < w ? u : w; }) - (1 << 20);
-    const bool fast = st[0] + wsp_max <= a.smax && st[1] + wlo_min >= -126;
+    // the result could be subnormal) the blocks are summed in fp64 by the slow kernel:
+    // exact while their scaled exponents span <= 34 bits, within fp32 rounding beyond.
+    // The decision is per head (the largest column spread of its q, k, v weight groups,
+    // uniform over the workgroup).
+    if constexpr (!SLOW) {
+      int gsp = 0, glo = 1 << 20;
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        const int g = s3 * a.H + h;
+        glo = min(glo, (int)a.gs[2 * g]);
+        gsp = max(gsp, (int)a.gs[2 * g + 1]);
+      }
+      if (!(st[0] + gsp <= a.smax && st[1] + glo >= -126)) {
+        if (threadIdx.x == 0) a.slow_list[atomicAdd(a.slow_count, 1)] = (b * a.ntb + tb) * a.H + h;
+        continue;  // uniform over the workgroup
+      }
+    }
     const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
     const float bb = (a.bias && colv) ? (PLAIN ? a.bias[jcol] : round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1)) : 0.0f;
     // the K loop and the epilogue, specialised on the accumulation (FAST: shifted int32;
@@ -175,34 +191,26 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
       typename std::conditional<FAST, int, double>::type acc[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0;
-      // Software pipeline over the K-blocks: the MFMA of block kb + 1 is issued before the
-      // epilogue of block kb, so the matrix core works while the VALU shifts and adds;
-      // the operands (weight codes: one coalesced 1-KB load per wave, x codes from the
-      // LDS tile, the column's block exponent) and the rows' exponent offsets ride one
-      // block further ahead.
-      auto ldw = [&](int kb) { return *reinterpret_cast<const v4i_*>(wp + kb * 1024); };
+      // Software pipeline over the K-blocks, unrolled by four so that every operand is
+      // loaded straight into the register it is consumed from (a rotating copy waits for
+      // the load it copies) and reloaded right after its use: the MFMA of block j + 1 is
+      // issued before the epilogue of block j, so the matrix core works while the VALU
+      // shifts and adds; the weight codes (one coalesced 1-KB load per wave) and the
+      // column's block exponent are loaded four blocks ahead, the rows' exponent offsets
+      // (LDS) one.  sched_barrier keeps this order (the scheduler otherwise sinks the
+      // MFMAs next to the loads they wait for).
+      auto ldw = [&](int kb) {
+        return __builtin_bit_cast(v4i_, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff, wsoff + kb * 1024, 0));
+      };
+      auto lew = [&](int kb) { return (int16_t)__builtin_amdgcn_raw_buffer_load_b16(ers, eoff, esoff + kb * 2, 0); };
       auto ldx = [&](int kb) { return *reinterpret_cast<const v4i_*>(xa + 32 * kb); };
       auto lde = [&](int kb, uint2 (&e)[4]) {
         const int16_t* eb = xe + kb * 32 + m0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) e[q] = *reinterpret_cast<const uint2*>(eb + 8 * q);  // rows 8q + m0 .. + 3
       };
-      const v16i zero = {};
-      v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ldx(0), ldw(0), zero, 0, 0, 0);
-      int16_t ecur = wep[0];
-      uint2 xcur[4];
-      lde(0, xcur);
-      const int k1 = nbk > 1 ? 1 : 0;
-      v4i_ an = ldx(k1), bn = ldw(k1);
-      int16_t en = wep[k1];
-      uint2 xn[4];
-      lde(k1, xn);
-      for (int kb = 0; kb < nbk; ++kb) {
-        const int k2 = kb + 2 < nbk ? kb + 2 : nbk - 1;
-        const v4i_ a2 = ldx(k2), b2 = ldw(k2);
-        const int16_t e2 = wep[k2];
-        const v16i cn = kb + 1 < nbk ? __builtin_amdgcn_mfma_i32_32x32x32_i8(an, bn, zero, 0, 0, 0) : c;
-        int ew = exp_from16(ecur);
+      auto epi = [&](const v16i& c, int16_t e16, const uint2 (&xcur)[4]) {
+        int ew = exp_from16(e16);
         cnan = cnan || ew == kExpNaN;
         ew = ew == kExpNaN ? wlo : ew;
         const int ewd = ew - wlo;
@@ -220,15 +228,61 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
             for (int r = 0; r < 4; ++r) acc[4 * q + r] += ldexp((double)c[4 * q + r], dx[r] + lo[r] + ew);
           }
         }
-        c = cn;
-        ecur = en;
-        en = e2;
-        an = a2;
-        bn = b2;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) xcur[q] = xn[q];
-        lde(k2, xn);
+      };
+      const v16i zero = {};
+      const int last = nbk - 1;
+      auto cl = [&](int kb) { return min(kb, last); };
+      auto mfma = [&](int kb, const v4i_& w) { return __builtin_amdgcn_mfma_i32_32x32x32_i8(ldx(kb), w, zero, 0, 0, 0); };
+      // slot s = block mod 4 (weights W*, column exponents E*); cA / cB the two products
+      // in flight, xA / xB their rows' exponent offsets
+      v4i_ W1 = ldw(cl(1)), W2 = ldw(cl(2)), W3 = ldw(cl(3));
+      int16_t E0 = lew(0), E1 = lew(cl(1)), E2 = lew(cl(2)), E3 = lew(cl(3));
+      v16i cA = mfma(0, ldw(0)), cB;
+      v4i_ W0 = ldw(cl(4));
+      uint2 xA[4], xB[4];
+      lde(0, xA);
+      // step: issue block j + 1 into cN (operand slot W, refilled with block j + 5), then
+      // the epilogue of block j from cP (exponent slot E, refilled with block j + 4)
+#define MXA_PROJ_STEP(cN, xN, W, cP, xP, E, j)              \
+  cN = mfma((j) + 1, W);                                   \
+  W = ldw(cl((j) + 5));                                    \
+  lde((j) + 1, xN);                                        \
+  __builtin_amdgcn_sched_barrier(0);                       \
+  epi(cP, E, xP);                                          \
+  E = lew(cl((j) + 4));                                    \
+  __builtin_amdgcn_sched_barrier(0);
+      // whole quads (blocks kb .. kb + 4 all real), one exit at the bottom
+      const int nquad = last >> 2;
+      int kb = 0;
+      for (int p = 0; p < nquad; ++p, kb += 4) {
+        MXA_PROJ_STEP(cB, xB, W1, cA, xA, E0, kb)
+        MXA_PROJ_STEP(cA, xA, W2, cB, xB, E1, kb + 1)
+        MXA_PROJ_STEP(cB, xB, W3, cA, xA, E2, kb + 2)
+        MXA_PROJ_STEP(cA, xA, W0, cB, xB, E3, kb + 3)
       }
+#undef MXA_PROJ_STEP
+      // the last 1 .. 4 blocks kb .. last (cA = block kb in flight)
+      const int r = nbk - kb;
+      if (r > 1) {
+        cB = mfma(kb + 1, W1);
+        lde(kb + 1, xB);
+      }
+      epi(cA, E0, xA);
+      if (r > 1) {
+        if (r > 2) {
+          cA = mfma(kb + 2, W2);
+          lde(kb + 2, xA);
+        }
+        epi(cB, E1, xB);
+      }
+      if (r > 2) {
+        if (r > 3) {
+          cB = mfma(kb + 3, W3);
+          lde(kb + 3, xB);
+        }
+        epi(cA, E2, xA);
+      }
+      if (r > 3) epi(cB, E3, xB);
       // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -------
       // branch-free: NaN by select; bb = 0 without a bias and o + 0 = o here (o is never
       // -0: an int32 sum converts to +0)
@@ -255,8 +309,7 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
         }
       }
     };
-    if (fast) run(std::integral_constant<bool, true>{});
-    else run(std::integral_constant<bool, false>{});
+    run(std::integral_constant<bool, !SLOW>{});
     __syncthreads();
     if (a.qkv_out) {  // the fp32 projection (tests): whole rows of the tile, coalesced
       for (int i = threadIdx.x; i < 32 * 3 * D; i += kThreads) {
@@ -306,6 +359,27 @@ __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MX
       cols_prep_column<PLAIN, PLAIN ? kF32 : -1>(a.cv, hrow_b + h, tb, c, xv, mx);
     }
     __syncthreads();
+  }
+}
+
+template <int NBD, bool PLAIN>
+__global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  proj_block<NBD, PLAIN, false>(a, blockIdx.x, blockIdx.y, (int)blockIdx.z * a.hpg,
+                                min(a.H, ((int)blockIdx.z + 1) * a.hpg), smem);
+}
+
+// the (token block, image, head) tiles qkv_proj_kernel listed: a fixed grid strides over
+// the list (its length is known on the device only; an empty list costs one read)
+template <int NBD, bool PLAIN>
+__global__ __launch_bounds__(64 * 3 * NBD) void qkv_proj_slow_kernel(ProjArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = __builtin_amdgcn_readfirstlane(*a.slow_count);
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int e = __builtin_amdgcn_readfirstlane(a.slow_list[i]);
+    const int h = e % a.H, t = e / a.H;
+    proj_block<NBD, PLAIN, true>(a, t % a.ntb, t / a.ntb, h, h + 1, smem);
+    __syncthreads();  // the next entry restages the LDS tile
   }
 }
 

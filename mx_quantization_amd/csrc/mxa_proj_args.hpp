@@ -10,13 +10,14 @@ namespace mxa {
 //       W[col n][32 kb + 16 h .. + 16] -- one coalesced 1-KB load per wave and K-block
 //   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
 //   ps  per padded column: smallest finite block exponent, spread (int16 pair)
+//   gs  per group (of gw real columns): the smallest ps exponent, the largest spread
 //   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
 //   hdr the geometry and settings it was prepared with (LinearWeightHeader, 256 B at
 //       offset 0, so a buffer of any size holds it): mxa_qkv_attention refuses a buffer
 //       whose header does not match the call instead of reading past its end
 struct LinearLayout {
   int G, NB32, nbk, Cpad;
-  int64_t hdr, pk, pe, ps, rawc, rawe, total;
+  int64_t hdr, pk, pe, ps, gs, rawc, rawe, total;
 };
 constexpr uint32_t kLinearWeightMagic = 0x5741584du;  // "MXAW"
 struct LinearWeightHeader {
@@ -44,6 +45,8 @@ __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int g
   o += al(pcols * L.nbk * 2);
   L.ps = o;
   o += al(pcols * 4);
+  L.gs = o;
+  o += al((int64_t)L.G * 4);
   L.rawc = o;
   o += al((int64_t)out_f * L.Cpad);
   L.rawe = o;
@@ -58,9 +61,13 @@ struct ProjArgs {
   const int8_t* pk;   // prepared weight (LinearLayout with gw = D)
   const int16_t* pe;
   const int16_t* ps;
+  const int16_t* gs;  // per weight group: smallest exponent, largest spread (the head's fast-path test)
+  int* slow_count;    // heads listed for qkv_proj_slow_kernel (zeroed before the launch)
+  int* slow_list;     // (b * ntb + tb) * H + h
   const float* bias;  // [3*H*D] or null
   float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
-  int B, N, H, D, nbk, Cpad, bfloat;
+  int B, N, H, D, nbk, Cpad, bfloat, ntb;
+  int pk_bytes, pe_bytes;  // buffer-descriptor extents of pk / pe (< 2 GiB: launch_proj checks)
   int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
   int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
   int autocast;  // 0, or the dtype torch.autocast rounds the product to before the fp32 bias add
