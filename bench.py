@@ -264,6 +264,8 @@ def stage_of_kernel(name):
         return "prep"
     if "qkv_proj_kernel" in name:
         return "proj"
+    if "mx_gemm" in name:
+        return "proj_linear"
     return None
 
 
@@ -426,6 +428,96 @@ def run_qkv(c, images, steps, warmup, device, world):
     return elapsed, stages, extra
 
 
+def run_qkv_proj(c, images, steps, warmup, device, world):
+    """x -> qkv mx.Linear -> attention -> proj mx.Linear in one call (mxa_attention_proj with
+    the qkv front end): the attention block's whole MX path from tokens to tokens, weights
+    prepared once outside the timed region.  Returns (elapsed, stage_ms, extra)."""
+    import torch
+    import mx_quantization_amd as M
+    from mx_quantization_amd import _native as N
+    B, H, Nt, D = len(images), c["H"], c["N"], c["D"]
+    C = H * D
+    rng = np.random.default_rng(98)
+    x = torch.from_numpy(rng.standard_normal((B, Nt, C), dtype=np.float32)).to(device)
+    W = torch.from_numpy((rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(C ** -0.5))).to(device)
+    bias = torch.from_numpy(rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.02)).to(device)
+    Wp = torch.from_numpy((rng.standard_normal((C, C), dtype=np.float32) * np.float32(C ** -0.5))).to(device)
+    bp = torch.from_numpy(rng.standard_normal(C, dtype=np.float32) * np.float32(0.02)).to(device)
+    wq, wp = M.LinearWeightMX(W, D), M.LinearWeightMX(Wp, C)
+    for _ in range(max(warmup, 1)):
+        y, idx = M.mx_qkv_attention(x, wq, bias, H, c["scale"], k_top=c["k"], pred_mode=c["mode"], proj_weight=wp,
+                                    proj_bias=bp)
+    torch.cuda.synchronize()
+    p = N.AttnParams()
+    p.B, p.H, p.N, p.T, p.D = B, H, Nt, Nt, D
+    p.k_top, p.scale = c["k"], float(np.float32(c["scale"]))
+    p.pred_mode, p.top_k, p.approx = N.PRED_MODES[c["mode"]], 1, 1
+    p.idx_out = idx.data_ptr()
+    xp = N.QkvParams()
+    xp.x, xp.x_row_stride, xp.C, xp.wq, xp.bias = x.data_ptr(), C, C, wq.buf.data_ptr(), bias.data_ptr()
+    pj = N.ProjParams()
+    pj.wq, pj.out_features, pj.bias = wp.buf.data_ptr(), C, bp.data_ptr()
+    yy = y.reshape(B * Nt, C)
+    pj.y, pj.y_row_stride = yy.data_ptr(), C
+    from mx_quantization_amd.ops import _workspace
+    ws = _workspace(device, N.lib().mxa_attention_proj_workspace_bytes(ctypes.byref(p), ctypes.byref(xp),
+                                                                       ctypes.byref(pj)))
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    stage_ms = (ctypes.c_float * N.PROJ_STAGES)()
+    stream = torch.cuda.current_stream(device).cuda_stream
+    elapsed = timed_region(
+        lambda: N.check(N.lib().mxa_attention_proj_timed(ctypes.byref(p), ctypes.byref(xp), ctypes.byref(pj), stream,
+                                                         steps, stage_ms), "mxa_attention_proj_timed"),
+        world, torch.cuda.synchronize, device)
+    stages = {name: float(stage_ms[slot]) for name, slot in zip(QKV_STAGES + ("proj_linear",), STAGE_SLOTS + (5,))}
+    ops = 2 * B * Nt * C * C  # int8 ops of the proj GEMM
+    pms = stages["proj_linear"]
+    extra = {"proj_linear_int8_tops": ops / (pms * 1e-3) / 1e12,
+             "proj_linear_frac_of_i8_peak": ops / (pms * 1e-3) / 1e12 / I8_PEAK_TOPS,
+             "proj_linear_min_bytes": B * Nt * C * (1 + 2 / 32) + C * C + B * Nt * C * 4,
+             "proj_input": "MX codes straight from the finishing kernel" if D % 32 == 0 else
+                           "fp32 workspace copy + row quantizer (a 32-block of C spans two heads)",
+             "fp32_attn_out_bytes_avoided": B * Nt * C * 4 * 2 if D % 32 == 0 else 0}
+    return elapsed, stages, extra
+
+
+def run_dropin(c, images, steps, warmup, device, world):
+    """The unchanged attention modules through install_dropin() (workloads/deit/scripts/
+    main.py:101-152 restated: mx.matmul QK^T, exponent_approximation operands, aQ @ aK^T,
+    the top-k in torch CPU order, gather / softmax / scatter, mx.matmul P.V): what a patched
+    module runs when only the imports change.  Returns (elapsed, extra)."""
+    import torch
+    import mx_quantization_amd as M
+    mx, funcs = M.install_dropin()
+    specs = {"w_elem_format": "int8", "a_elem_format": "int8", "scale_bits": 8, "shared_exp_method": "max",
+             "block_size": 32, "bfloat": 32, "round": "nearest", "round_mx_output": "nearest",
+             "round_output": "nearest", "round_weight": "nearest", "mx_flush_fp32_subnorms": False}
+    t = lambda a: torch.from_numpy(a).to(device)
+    q, k, v, _ = (None if a is None else t(a) for a in make_inputs(c, images))
+
+    def step():
+        ts = mx.matmul(q, k.transpose(-2, -1), mx_specs=specs, mode_config="aa") * c["scale"]
+        aq, ak = funcs.exponent_approximation(Q=q, K=k, mx_specs=specs).exponent_based_sign()
+        pred = aq @ ak.transpose(-2, -1)
+        _, idx = M.topk(pred, c["k"])
+        vals = ts.gather(dim=-1, index=idx)
+        attn = torch.zeros_like(ts)
+        attn.scatter_(-1, idx, torch.softmax(vals, dim=-1).to(attn.dtype))
+        return mx.matmul(attn, v, mx_specs=specs, mode_config="aa"), idx
+
+    for _ in range(max(warmup, 1)):
+        out, idx = step()
+    torch.cuda.synchronize()
+
+    def timed():
+        for _ in range(steps):
+            step()
+    elapsed = timed_region(timed, world, torch.cuda.synchronize, device)
+    ref_out, ref_idx = M.mx_topk_attention(q, k, v, c["scale"], k_top=c["k"], pred_mode=c["mode"])
+    return elapsed, {"idx_equal_fused": bool(torch.equal(idx, ref_idx)),
+                     "out_max_abs_diff_vs_fused": float((out - ref_out).abs().max())}
+
+
 def run_secondary(args, c, rank, world, images, lines, run, device, res=None):
     """The secondary lines: `qkv` (the config's fused qkv-Linear line) and `dit` (the
     DiT-XL/2 line of deit_base).  With res None (no main line: profiling passes) the
@@ -444,6 +536,25 @@ def run_secondary(args, c, rank, world, images, lines, run, device, res=None):
              "attention core's MX operands, then the same attention" % (c["H"] * c["D"]),
              "value": qtok / qel, "unit": "tokens/s", "ms_per_step": qel / qsteps * 1e3, "stages_ms": qst, **qex})
 
+    if args.config in ("deit_base", "dit_xl2") and "qkvproj" in lines and run is run_config:
+        # ... and the proj mx.Linear behind it (both halves): x -> y
+        psteps = max(args.steps // 2, 1)
+        pel, pst, pex = run_qkv_proj(c, images, psteps, 2, device, world)
+        ptok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * psteps
+        res.setdefault("secondary", []).append(
+            {"config": args.config + "+qkv_linear+proj_linear", "workload": "x (B, N, C=%d) -> qkv mx.Linear -> MX "
+             "top-k attention -> proj mx.Linear -> y (B, N, C), one call" % (c["H"] * c["D"]),
+             "value": ptok / pel, "unit": "tokens/s", "ms_per_step": pel / psteps * 1e3, "stages_ms": pst, **pex})
+    if args.config == "deit_base" and "dropin" in lines and run is run_config:
+        # the drop-in modules the unchanged attention code imports (install_dropin)
+        dsteps = max(args.steps // 4, 1)
+        del_, dex = run_dropin(c, images, dsteps, 1, device, world)
+        dtok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * dsteps
+        res.setdefault("secondary", []).append(
+            {"config": "deit_base+dropin", "workload": "the unchanged DeiT attention glue (main.py:101-152) on the "
+             "install_dropin() mx / funcs modules: mx.matmul QK^T and P.V on the block-scaled MFMA GEMM, "
+             "exponent_approximation operands, torch-CPU-order top-k; torch gather / softmax / scatter",
+             "value": dtok / del_, "unit": "tokens/s", "ms_per_step": del_ / dsteps * 1e3, **dex})
     if args.config == "deit_base" and "dit" in lines:
         d = CONFIGS["dit_xl2"]
         dimg = shard(d, rank, world, args.scaling)
@@ -495,8 +606,9 @@ def main(argv=None, run=run_config):
     ap.add_argument("--pmc-json", default=None,
                     help="PMC instruction counters per kernel (tools/pmc_summary.py --json; default: the "
                          "committed profiles/<PROFILE_TAG>_pmc_<config>.json)")
-    ap.add_argument("--lines", default="main,qkv,dit",
-                    help="which lines to run: main (the config), qkv (its fused qkv-Linear line), dit "
+    ap.add_argument("--lines", default="main,qkv,qkvproj,dropin,dit",
+                    help="which lines to run: main (the config), qkv (its fused qkv-Linear line), qkvproj (x -> "
+                         "qkv Linear -> attention -> proj Linear), dropin (the drop-in modules' path), dit "
                          "(the DiT-XL/2 secondary of deit_base)")
     args = ap.parse_args(argv)
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MXA_ABI_VERSION 3
+#define MXA_ABI_VERSION 4
 
 /* status codes */
 #define MXA_OK 0
@@ -253,6 +253,54 @@ int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* x, hipStre
 /* mxa_attention_timed for the fused projection path (stage 0 = x quantize + projection) */
 int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_params* x, hipStream_t stream, int32_t iters,
                             float* stage_ms);
+
+/*
+ * mx.Linear forward (microxscaling/mx/linear.py:20-103) on a prepared weight:
+ *   out = bf(fl32(MX(bf(x), along in_features) @ MX(bf(W), along in_features)^T));
+ *   out = bf(out + bf(bias))          (bf = quantize_elemwise_op: bfloat rounding or none)
+ * x (rows, in_features) fp32 at x_row_stride; wq from mxa_linear_weight_prep(W, out_features,
+ * in_features, any group_width, flush_subnormals, bfloat) -- MXA_ERR_ARG if its header
+ * differs; out (rows, out_features) fp32 at out_row_stride.  Every product is the exact sum
+ * rounded once (the reference's MKL sgemm order is unpinned: equal within fp32 rounding).
+ * autocast_dtype: 0, or MXA_DT_F16 / BF16 (torch.autocast: the product rounded to that
+ * dtype before the fp32 bias add).  The patched modules' proj Linear (deit main.py:154, DiT
+ * models.py:227) and every Linear of the mx.Linear drop-in.
+ */
+int64_t mxa_linear_workspace_bytes(int64_t rows, int32_t in_features, int32_t out_features);
+int mxa_linear(const float* x, int64_t rows, int32_t in_features, int64_t x_row_stride, const void* wq,
+               int32_t out_features, const float* bias, float* out, int64_t out_row_stride,
+               int32_t flush_subnormals, int32_t bfloat, int32_t autocast_dtype, void* workspace,
+               int64_t workspace_bytes, hipStream_t stream);
+
+/*
+ * The attention core with the proj Linear fused behind it: the patched modules'
+ *   x = attn_out.transpose(1, 2).reshape(B, N, C);  x = self.proj(x)
+ * (workloads/deit/scripts/main.py:152-154, workloads/DiT/models.py:225-227; proj an
+ * mx.Linear, microxscaling/mx/linear.py:20-103) after mxa_attention (xq == NULL) or
+ * mxa_qkv_attention (xq != NULL).  With D % 32 == 0 (float32, no autocast) the finishing
+ * kernel MX-quantizes each 32-column P.V tile straight into the proj's input codes -- the
+ * fp32 attention output never reaches HBM; otherwise (a 32-element block of C spans two
+ * heads) the output goes through a workspace copy and the row quantizer.  p->out is not
+ * written (may be NULL); y (B*N, out_features) fp32 at y_row_stride.  Top-k path only.
+ */
+typedef struct mxa_proj_params {
+  const void* wq;        /* mxa_linear_weight_prep output for W_proj (out_features, H*D)      */
+  int32_t out_features;
+  const float* bias;     /* (out_features) or null                                           */
+  float* y;              /* (B*N, out_features) rows at y_row_stride                         */
+  int64_t y_row_stride;
+} mxa_proj_params;
+
+int64_t mxa_attention_proj_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* xq,
+                                           const mxa_proj_params* pj);
+int mxa_attention_proj(const mxa_attn_params* p, const mxa_qkv_params* xq, const mxa_proj_params* pj,
+                       hipStream_t stream);
+/* mxa_attention_timed for it: stage_ms[MXA_PROJ_STAGES] -- slots 0..4 as mxa_attention_timed
+ * (slot 0 the x quantize + qkv projection when xq != NULL), slot 5 the proj Linear (with
+ * the row quantizer when the output went through the workspace) */
+#define MXA_PROJ_STAGES 6
+int mxa_attention_proj_timed(const mxa_attn_params* p, const mxa_qkv_params* xq, const mxa_proj_params* pj,
+                             hipStream_t stream, int32_t iters, float* stage_ms);
 
 /*
  * mx.matmul forward (microxscaling/mx/matmul.py:31-100, :211-222): in1 (batch, M, K)

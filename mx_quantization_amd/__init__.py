@@ -21,9 +21,11 @@ from .ops import (  # noqa: F401
     elsa_cos_table,
     mx_approx_scores,
     LinearWeightMX,
+    mx_linear,
     mx_matmul,
     mx_qkv_attention,
     mx_topk_attention,
+    mx_topk_attention_proj,
     quantize_bfloat,
     quantize_mx,
     shared_exponents,
@@ -31,7 +33,7 @@ from .ops import (  # noqa: F401
     unpack_mask,
 )
 
-__all__ = ["mx_topk_attention", "mx_qkv_attention", "LinearWeightMX", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
+__all__ = ["mx_topk_attention", "mx_qkv_attention", "mx_topk_attention_proj", "mx_linear", "LinearWeightMX", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
 
 
 def install_dropin():

@@ -21,7 +21,7 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
-ABI_VERSION = 3
+ABI_VERSION = 4
 DT_F32, DT_F16, DT_BF16 = 0, 1, 2
 DTYPES = {torch.float32: DT_F32, torch.float16: DT_F16, torch.bfloat16: DT_BF16}
 PATH_NAMES = {2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
@@ -53,6 +53,13 @@ class QkvParams(ctypes.Structure):
                 ("qkv_out", c_vp), ("autocast_dtype", c_i32)]
 
 
+class ProjParams(ctypes.Structure):
+    """mirror of struct mxa_proj_params (include/mxa.h)"""
+    _fields_ = [("wq", c_vp), ("out_features", c_i32), ("bias", c_vp), ("y", c_vp), ("y_row_stride", c_i64)]
+
+
+PROJ_STAGES = 6  # MXA_PROJ_STAGES
+
 _SIGS = {
     "mxa_abi_version": (c_i32, []),
     "mxa_status_string": (ctypes.c_char_p, [c_i32]),
@@ -73,6 +80,15 @@ _SIGS = {
     "mxa_qkv_attention": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp]),
     "mxa_qkv_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), c_vp, c_i32,
                                         ctypes.POINTER(c_f32)]),
+    "mxa_linear_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32]),
+    "mxa_linear": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_i64,
+                           c_vp]),
+    "mxa_attention_proj_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams),
+                                                   ctypes.POINTER(ProjParams)]),
+    "mxa_attention_proj": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams), ctypes.POINTER(ProjParams),
+                                   c_vp]),
+    "mxa_attention_proj_timed": (c_i32, [ctypes.POINTER(AttnParams), ctypes.POINTER(QkvParams),
+                                         ctypes.POINTER(ProjParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                            c_i32, c_i32, c_i32, c_vp, c_i64, c_vp]),
     "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),

@@ -17,13 +17,16 @@ LIB = os.path.join(HERE, "libmxa.so")
 # selection kernel's instantiations each (MXA_SEL_PART), so that the parts build in parallel
 UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", "", ("MXA_SEL_PART=0",)),
          ("mxa_sel.hip", "_p1", ("MXA_SEL_PART=1",)), ("mxa_sel.hip", "_p2", ("MXA_SEL_PART=2",)),
-         ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ())]
+         ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
-           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
+           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
            "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+OBJDIR = os.path.join(HERE, "build")  # per-unit objects + dependency files (git-ignored)
 
 
 def _stale(lib=LIB):
@@ -34,23 +37,48 @@ def _stale(lib=LIB):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _obj_stale(obj, dep, cmd_file, cmd):
+    """An object is rebuilt when it, its dependency list or its command line is missing or
+    older than any file the compiler read for it (hipcc -MD)."""
+    if not (os.path.exists(obj) and os.path.exists(dep) and os.path.exists(cmd_file)):
+        return True
+    with open(cmd_file) as f:
+        if f.read() != " ".join(cmd):
+            return True
+    with open(dep) as f:
+        files = f.read().replace("\\\n", " ").split()
+    t = os.path.getmtime(obj)
+    files = [x for x in files[1:] if not x.endswith(":")]
+    return any(not os.path.exists(x) or os.path.getmtime(x) > t for x in files + [os.path.abspath(__file__)])
+
+
 def build(force=False, verbose=True, defines=(), tag=""):
     """defines / tag: a tools-only variant (e.g. defines=("MXA_SEL_SKIP=1",), tag="skip1"
-    -> libmxa_skip1.so, loaded by tools through MXA_LIB); never the product."""
+    -> libmxa_skip1.so, loaded by tools through MXA_LIB); never the product.  Units whose
+    object is up to date (by hipcc's dependency list) are not recompiled unless force."""
     lib = LIB.replace("libmxa.so", f"libmxa_{tag}.so") if tag else LIB
     if not force and not _stale(lib):
         return lib
+    os.makedirs(OBJDIR, exist_ok=True)
     objs, procs = [], []
     for src, suffix, unit_defs in UNITS:  # one hipcc per translation unit, in parallel
-        obj = os.path.join(CSRC, src.replace(".hip", f"{suffix}{'_' + tag if tag else ''}.o"))
+        stem = src.replace(".hip", f"{suffix}{'_' + tag if tag else ''}")
+        obj, dep = os.path.join(OBJDIR, stem + ".o"), os.path.join(OBJDIR, stem + ".d")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                "-Wall", "-Wno-unused-function", "-I", os.path.join(HERE, "..", "include"),
                "-c", os.path.join(CSRC, src), "-o", obj] + [f"-D{d}" for d in tuple(unit_defs) + tuple(defines)]
+        objs.append(obj)
+        cmd_file = obj + ".cmd"
+        if not force and not _obj_stale(obj, dep, cmd_file, cmd):
+            continue
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-    bad = [p.args for p in procs if p.wait() != 0]
+        procs.append((subprocess.Popen(cmd + ["-MD", "-MF", dep]), cmd, cmd_file))
+    bad = [c for p, c, _ in procs if p.wait() != 0]
+    for p, c, cf in procs:
+        if p.returncode == 0:
+            with open(cf, "w") as f:
+                f.write(" ".join(c))
     if bad:
         raise subprocess.CalledProcessError(1, bad[0])
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
@@ -58,8 +86,6 @@ def build(force=False, verbose=True, defines=(), tag=""):
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(lib + ".tmp", lib)
-    for o in objs:
-        os.remove(o)
     return lib
 
 

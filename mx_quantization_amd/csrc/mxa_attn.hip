@@ -44,38 +44,6 @@ __global__ void selftest_mfma32_kernel(const int8_t* A, const int8_t* B, int32_t
   for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + m0 + (i & 3)) * 32 + ln] = c[i];
 }
 
-// ---- mx.matmul: C[b] = MX(A[b], along K) @ MX(B[b], along K) ---------------
-struct MatmulArgs {
-  const int8_t* ac;
-  const int16_t* as;
-  const int8_t* bt;
-  const int16_t* bsc;
-  int M, Nc, nbk, kpad, bfloat, dt;
-  void* c;  // dtype dt
-};
-
-__global__ __launch_bounds__(256) void matmul_kernel(MatmulArgs a) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t bt = blockIdx.z;
-  const int row0 = blockIdx.y * 16;
-  const int col0 = (blockIdx.x * 4 + wave) * 16;
-  if (col0 >= a.Nc) return;
-  const int rows_valid = min(16, a.M - row0);
-  const int cols_valid = min(16, a.Nc - col0);
-  const int64_t arow0 = bt * a.M + row0;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  scaled_tile<false>(a.ac + arow0 * a.kpad, a.kpad, rows_valid, a.as + arow0 * a.nbk, a.nbk, 1,
-                     a.bt + (bt * a.Nc + col0) * a.kpad, a.kpad, cols_valid, a.bsc + bt * a.nbk * a.Nc + col0,
-                     1, a.Nc, a.nbk, acc);
-  const int col = col0 + (lane & 15);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 4 * (lane >> 4) + i;
-    if (r < rows_valid && col < a.Nc)
-      store_dt(a.c, (arow0 + r) * a.Nc + col, round_bfloat(round_dt((float)acc[i], a.dt), a.bfloat, kRoundNearest, 1, a.dt), a.dt);
-  }
-}
-
 __global__ void selftest_mfma_kernel(const int8_t* A, const int8_t* B, int32_t* C) {
   // A row-major 16x32, B row-major 32x16 (k-major), C row-major 16x16
   const int lane = threadIdx.x;
@@ -104,6 +72,8 @@ struct AttnLayout {
   int nbd, dpad, ntb, tpad;
   int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx32;
   int64_t xc, xs, slow;  // fused qkv projection: x codes / exponents, slow-head list
+  int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
+                              // copy (D % 32 != 0 only), the GEMM's fp64 wave list
   int64_t total;
 };
 
@@ -119,7 +89,13 @@ int score_mode(const mxa_attn_params* p, bool ranked) {
   }
 }
 
-AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params* xq = nullptr) {
+// the proj Linear's input comes MX-quantized out of the finishing kernel
+bool proj_codes_direct(const mxa_attn_params* p) {
+  return p->D % 32 == 0 && p->dtype == MXA_DT_F32 && p->score_dtype <= MXA_DT_F32;
+}
+
+AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params* xq = nullptr,
+                       const mxa_proj_params* pj = nullptr) {
   AttnLayout L{};
   const int64_t BH = (int64_t)p->B * p->H;
   L.nbd = (p->D + 31) / 32;
@@ -158,6 +134,13 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
     L.xc = take(tokens * nbk * 32);
     L.xs = take(tokens * nbk * 2);
     L.slow = take(4 * (1 + (int64_t)L.ntb * p->B * p->H));  // count, then the entries
+  }
+  if (pj) {
+    const int64_t C = (int64_t)p->H * p->D, nbk = (C + 31) / 32, tokens = (int64_t)p->B * p->N;
+    L.yc = take(tokens * nbk * 32);
+    L.ys = take(tokens * nbk * 2);
+    L.yf = take(proj_codes_direct(p) ? 0 : tokens * C * 4);
+    L.yslow = take(gemm_slow_bytes((int)std::min<int64_t>(tokens, INT32_MAX), pj->out_features, 1));
   }
   L.total = off;
   return L;
@@ -229,15 +212,22 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
 // plan != nullptr: only report the kernel path (MXA_PATH_*), launch nothing;
 // scores_only: the approximate (or true) scores into p->pred_out / true_out, no top-k
 // xq: the fused qkv projection (q, k, v produced from x and the prepared weight)
+// pj: the proj Linear behind the attention (y = mx.Linear(out.transpose(1,2).reshape(B,N,C)))
 static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr,
-                          bool scores_only = false, const mxa_qkv_params* xq = nullptr) {
+                          bool scores_only = false, const mxa_qkv_params* xq = nullptr,
+                          const mxa_proj_params* pj = nullptr) {
   if (!p) return MXA_ERR_ARG;
+  if (pj) {
+    if (scores_only || !p->top_k || !pj->wq || !pj->y || pj->out_features <= 0 || pj->y_row_stride < pj->out_features)
+      return MXA_ERR_ARG;
+    if ((int64_t)p->B * p->N > INT32_MAX) return MXA_ERR_UNSUPPORTED;
+  }
   if (xq) {
     if (!xq->x || !xq->wq || xq->C <= 0 || xq->x_row_stride < xq->C || p->N != p->T || scores_only) return MXA_ERR_ARG;
   } else if (!p->q || !p->k) {
     return MXA_ERR_ARG;
   }
-  if (!scores_only && ((!p->v && !xq) || !p->out)) return MXA_ERR_ARG;
+  if (!scores_only && ((!p->v && !xq) || (!p->out && !pj))) return MXA_ERR_ARG;
   if (scores_only && !(p->approx ? p->pred_out : p->true_out)) return MXA_ERR_ARG;
   if (p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0) return MXA_ERR_ARG;
   if (!scores_only && p->top_k && (p->k_top <= 0 || p->k_top > p->T)) return MXA_ERR_ARG;
@@ -258,6 +248,9 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
                                                                 p->bfloat),
                                   stream))
     return MXA_ERR_ARG;
+  if (pj && !linear_weight_verify_any_group(pj->wq, pj->out_features, p->H * p->D, p->flush_subnormals, p->bfloat,
+                                            stream))
+    return MXA_ERR_ARG;
   mxa_attn_params pp = *p;
   if (scores_only) {  // the selection kernel alone, with no kept keys
     pp.top_k = 0;
@@ -269,7 +262,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   const bool ranked = topk || scores_only;  // the selection kernel runs
   const int mode = score_mode(&pp, ranked);
   if (mode == kModeElsa && (!pp.elsa_proj || pp.N != pp.T)) return MXA_ERR_ARG;  // elsa_approximation.py:126, :142
-  const AttnLayout L = attn_layout(&pp, mode, xq);
+  const AttnLayout L = attn_layout(&pp, mode, xq, pj);
   const int64_t BH = (int64_t)pp.B * pp.H;
 
   int opq = MXA_OP_SIGN, opk = MXA_OP_SIGN;
@@ -387,6 +380,16 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.out = pp.out; r2.os0 = pp.out_strides[0]; r2.os1 = pp.out_strides[1]; r2.os2 = pp.out_strides[2];
   r2.idx_out = pp.idx_out; r2.true_out = pp.true_out; r2.pred_out = pp.pred_out; r2.mask_out = pp.mask_out;
   r2.idx32 = reinterpret_cast<int32_t*>(ws + L.idx32);
+  const bool direct = pj && proj_codes_direct(&pp);
+  if (direct) {  // the finishing kernel writes the proj's input codes
+    r2.xo_codes = reinterpret_cast<int8_t*>(ws + L.yc);
+    r2.xo_exps = reinterpret_cast<int16_t*>(ws + L.ys);
+  } else if (pj) {  // fp32 (B, N, H*D) into the workspace, then the row quantizer
+    r2.out = ws + L.yf;
+    r2.os0 = (int64_t)pp.N * pp.H * pp.D; r2.os1 = pp.D; r2.os2 = (int64_t)pp.H * pp.D;
+    r2.s_dt = MXA_DT_F32;
+    if (pp.dtype != MXA_DT_F32 || pp.score_dtype > MXA_DT_F32) return MXA_ERR_UNSUPPORTED;
+  }
   if (ranked) {
     rc = launch_select(r2, mode, (int)BH, stream, false);
     if (rc) return rc;
@@ -397,6 +400,26 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
     if (rc) return rc;
   }
   if (ev) (void)hipEventRecord(ev[5], stream);
+  if (pj) {
+    const int C = pp.H * pp.D, nbk = (C + 31) / 32;
+    const int64_t tokens = (int64_t)pp.B * pp.N;
+    int8_t* yc = reinterpret_cast<int8_t*>(ws + L.yc);
+    int16_t* ys = reinterpret_cast<int16_t*>(ws + L.ys);
+    if (!direct) {
+      RowsPrepArgs ry{};
+      ry.x = ws + L.yf; ry.s0 = 0; ry.s1 = 0; ry.s2 = C;
+      ry.H = 1; ry.R = tokens; ry.rows = tokens; ry.D = C; ry.nb = nbk; ry.dpad = 32 * nbk;
+      ry.vec4 = C % 4 == 0;
+      ry.op_kind = MXA_OP_MXINT8; ry.flush = pp.flush_subnormals; ry.bfloat = pp.bfloat; ry.dt = MXA_DT_F32;
+      ry.codes = yc; ry.sT = ys;
+      rc = launch_rows_prep(ry, stream);
+      if (rc) return rc;
+    }
+    rc = launch_linear_codes(yc, ys, tokens, C, pj->wq, pj->out_features, pj->bias, pj->y, pj->y_row_stride,
+                             pp.bfloat, 0, reinterpret_cast<int*>(ws + L.yslow), stream);
+    if (rc) return rc;
+    if (ev) (void)hipEventRecord(ev[6], stream);
+  }
   return MXA_OK;
 }
 
@@ -408,6 +431,28 @@ extern "C" int64_t mxa_qkv_attention_workspace_bytes(const mxa_attn_params* p, c
 extern "C" int mxa_qkv_attention(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream) {
   if (!xq) return MXA_ERR_ARG;
   return attention_impl(p, stream, nullptr, nullptr, false, xq);
+}
+
+static int timed_impl(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream, int32_t iters,
+                      float* stage_ms, const mxa_proj_params* pj);
+
+extern "C" int64_t mxa_attention_proj_workspace_bytes(const mxa_attn_params* p, const mxa_qkv_params* xq,
+                                                      const mxa_proj_params* pj) {
+  if (!p || !pj || p->B <= 0 || p->H <= 0 || p->N <= 0 || p->T <= 0 || p->D <= 0 || pj->out_features <= 0) return -1;
+  if (xq && xq->C <= 0) return -1;
+  return attn_layout(p, score_mode(p, true), xq, pj).total;
+}
+
+extern "C" int mxa_attention_proj(const mxa_attn_params* p, const mxa_qkv_params* xq, const mxa_proj_params* pj,
+                                  hipStream_t stream) {
+  if (!pj) return MXA_ERR_ARG;
+  return attention_impl(p, stream, nullptr, nullptr, false, xq, pj);
+}
+
+extern "C" int mxa_attention_proj_timed(const mxa_attn_params* p, const mxa_qkv_params* xq, const mxa_proj_params* pj,
+                                        hipStream_t stream, int32_t iters, float* stage_ms) {
+  if (!pj) return MXA_ERR_ARG;
+  return timed_impl(p, xq, stream, iters, stage_ms, pj);
 }
 
 extern "C" int mxa_approx_scores(const mxa_attn_params* p, hipStream_t stream) {
@@ -425,21 +470,22 @@ extern "C" int mxa_attention_path(const mxa_attn_params* p) {
 }
 
 static int timed_impl(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream, int32_t iters,
-                      float* stage_ms) {
+                      float* stage_ms, const mxa_proj_params* pj) {
   if (iters <= 0 || !stage_ms) return MXA_ERR_ARG;
-  std::vector<hipEvent_t> ev((size_t)iters * MXA_ATTN_STAGES_PLUS1);
+  const int ns = pj ? MXA_PROJ_STAGES : MXA_ATTN_STAGES, ne = ns + 1;
+  std::vector<hipEvent_t> ev((size_t)iters * ne);
   for (auto& e : ev)
     if (hipEventCreate(&e) != hipSuccess) return MXA_ERR_LAUNCH;
   int rc = MXA_OK;
   for (int i = 0; i < iters && rc == MXA_OK; ++i)
-    rc = attention_impl(p, stream, &ev[(size_t)i * MXA_ATTN_STAGES_PLUS1], nullptr, false, xq);
+    rc = attention_impl(p, stream, &ev[(size_t)i * ne], nullptr, false, xq, pj);
   if (rc == MXA_OK && hipStreamSynchronize(stream) != hipSuccess) rc = MXA_ERR_LAUNCH;
   if (rc == MXA_OK) {
-    for (int s = 0; s < MXA_ATTN_STAGES; ++s) {
+    for (int s = 0; s < ns; ++s) {
       double acc = 0.0;
       for (int i = 0; i < iters; ++i) {
         float ms = 0.0f;
-        (void)hipEventElapsedTime(&ms, ev[(size_t)i * MXA_ATTN_STAGES_PLUS1 + s], ev[(size_t)i * MXA_ATTN_STAGES_PLUS1 + s + 1]);
+        (void)hipEventElapsedTime(&ms, ev[(size_t)i * ne + s], ev[(size_t)i * ne + s + 1]);
         acc += ms;
       }
       stage_ms[s] = (float)(acc / iters);
@@ -450,20 +496,20 @@ static int timed_impl(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStr
 }
 
 extern "C" int mxa_attention_timed(const mxa_attn_params* p, hipStream_t stream, int32_t iters, float* stage_ms) {
-  return timed_impl(p, nullptr, stream, iters, stage_ms);
+  return timed_impl(p, nullptr, stream, iters, stage_ms, nullptr);
 }
 
 extern "C" int mxa_qkv_attention_timed(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream,
                                        int32_t iters, float* stage_ms) {
   if (!xq) return MXA_ERR_ARG;
-  return timed_impl(p, xq, stream, iters, stage_ms);
+  return timed_impl(p, xq, stream, iters, stage_ms, nullptr);
 }
 
 extern "C" int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc) {
   if (batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return -1;
   const int64_t nbk = (K + 31) / 32, kpad = nbk * 32;
   return align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) + align_up(batch * Nc * kpad) +
-         align_up(batch * nbk * Nc * 2);
+         align_up(batch * nbk * Nc * 2) + gemm_slow_bytes(M, Nc, std::min<int64_t>(batch, 65535));
 }
 
 extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
@@ -501,10 +547,18 @@ extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, 
   cb.codes_t = bt; cb.scale = bsc;
   rc = launch_cols_prep(cb, stream);
   if (rc) return rc;
-  MatmulArgs ma{ac, as, bt, bsc, M, Nc, nbk, kpad, bfloat, c_dtype, c};
-  dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 15) / 16), (unsigned)batch);
-  hipLaunchKernelGGL(matmul_kernel, grid, dim3(256), 0, stream, ma);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+  // C[b] = MX(A[b]) @ MX(B[b]) on the block-scaled GEMM (mxa_gemm.hpp): A's MX codes
+  // row-major along K, B's transposed codes [Nc][kpad], exponents [nbk][Nc]
+  GemmArgs g{};
+  g.a = ac; g.ae = as; g.a_bat = (int64_t)M * kpad; g.ae_bat = (int64_t)M * nbk; g.lda = kpad;
+  g.b = bt; g.b_bat = (int64_t)Nc * kpad; g.ldb = kpad;
+  g.be = bsc; g.be_bat = (int64_t)nbk * Nc; g.be_n = 1; g.be_k = Nc;
+  g.M = M; g.Nc = Nc; g.nbk = nbk;
+  g.linear = 0; g.dt = c_dtype; g.bfloat = bfloat;
+  g.c = c; g.c_bat = (int64_t)M * Nc; g.ldc = Nc;
+  int* slow = reinterpret_cast<int*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) +
+                                     align_up(batch * Nc * kpad) + align_up(batch * nbk * Nc * 2));
+  return launch_gemm(g, batch, slow, stream);
 }
 
 extern "C" int mxa_selftest_mfma32(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream) {

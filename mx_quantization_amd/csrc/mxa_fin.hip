@@ -48,7 +48,8 @@ static bool finish_pair(const Rows2Args& ra) { return ra.k_top <= 32; }
 static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg) {
   const int tiles = (ra.N + kFinTile - 1) / kFinTile;
   const bool pair = finish_pair(ra);
-  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, pair).total; };
+  const bool xo = ra.xo_codes != nullptr;
+  auto lds = [&](int w) { return fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, pair, xo).total; };
   if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   // a head's tiles round-robin over the waves of one workgroup (the K / V tables
   // staged once per head); few heads (PixArt cross-attention): the tiles split over
@@ -74,21 +75,25 @@ static int finish_plan(const Rows2Args& ra, int BH, int* waves, int* rows_per_wg
   *rows_per_wg = kFinTile * ((tiles + chunks - 1) / chunks);
   return MXA_OK;
 }
-template <int NB, int KS, bool PAIR, bool XDT>
+template <int NB, int KS, bool PAIR, bool XDT, bool XO = false>
 static int launch_finish_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
   int rc = finish_plan(ra, BH, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
-  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR).total;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR, XDT>),
+  const size_t lds = fin_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, PAIR, XO).total;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel<NB, KS, PAIR, XDT, XO>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR, XDT>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  hipLaunchKernelGGL((finish_kernel<NB, KS, PAIR, XDT, XO>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 template <int NB, int KS, bool PAIR>
 static int launch_finish_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (ra.xo_codes) {  // output MX codes for the proj Linear: float32, D % 32 == 0
+    if (ra.s_dt != kF32 || ra.in_dt != kF32 || ra.D % 32) return MXA_ERR_UNSUPPORTED;
+    return launch_finish_xdt<NB, KS, PAIR, false, true>(ra, BH, stream);
+  }
   if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish_xdt<NB, KS, PAIR, true>(ra, BH, stream);
   return launch_finish_xdt<NB, KS, PAIR, false>(ra, BH, stream);
 }

@@ -22,6 +22,7 @@
 // workloads/deit/scripts/main.py:124-152, workloads/DiT/models.py:195-225,
 // workloads/PixArt/models/MX_transformer_block.py:679-717, :826-859.
 #pragma once
+#include "mxa_prep.hpp"
 #include "mxa_select.hpp"
 
 namespace mxa {
@@ -34,9 +35,11 @@ typedef int v4i_ __attribute__((ext_vector_type(4)));
 // LDS layout: tables, then per wave the P code tile [32][vst], the P block scales
 // sP [ntb][32] (float), the block maxima bm [4][16] (u32, one DPP row each)
 struct FinLds {
-  size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
+  size_t kc, ke, vt, ve, waves, per_wave, sp, bm, ot, total;
 };
-__host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves, bool pair) {
+// xo: + the 32 x 32 fp32 output block being MX-quantized for the proj Linear
+__host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves, bool pair,
+                                          bool xo = false) {
   FinLds L;
   size_t o = 0;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -51,7 +54,8 @@ __host__ __device__ inline FinLds fin_lds(int T, int D, int kst, int nbd, int vs
   L.waves = o;
   L.sp = al((size_t)kFinTile * vst);
   L.bm = L.sp + al((size_t)ntb * kFinTile * 4);
-  L.per_wave = L.bm + (pair ? 32 : 4) * 16 * 4;  // block maxima: 16 per row of a pass
+  L.ot = L.bm + (pair ? 32 : 4) * 16 * 4;  // block maxima: 16 per row of a pass
+  L.per_wave = L.ot + (xo ? kFinTile * 33 * 4 : 0);
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
@@ -69,7 +73,9 @@ __device__ __forceinline__ float scale_f(int e) {
 //   tile instead of eight.
 // XDT: float16 / bfloat16 inputs or scores (include/mxa.h dtype / score_dtype): the
 // dtype roundings at run time; XDT = false compiles them away (the float32 path).
-template <int NB, int KS, bool PAIR, bool XDT>
+// XO: the output goes to the proj Linear as MX codes along C (Rows2Args::xo_codes;
+// float32, D % 32 == 0: every 32-column P.V tile is one MX block of the output row)
+template <int NB, int KS, bool PAIR, bool XDT, bool XO = false>
 __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   const int T = a.T, D = a.D, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
   constexpr int nbd = NB;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves, PAIR);
+  const FinLds L = fin_lds(T, D, kst, nbd, vst, ntb, a.waves, PAIR, XO);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
   int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
@@ -344,6 +350,29 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
           acc[4 * q + 2] = fmaf((float)c[4 * q + 2], s4.z * sv, acc[4 * q + 2]);
           acc[4 * q + 3] = fmaf((float)c[4 * q + 3], s4.w * sv, acc[4 * q + 3]);
         }
+      }
+      if constexpr (XO) {
+        // ---- 3'. the 32 x 32 block -> MX codes of block (h D + dt) / 32 of each output
+        // row (what rows_prep makes of the (B, N, C) output for the proj Linear) -------
+        float* ot = reinterpret_cast<float*>(wb + L.ot);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          ot[(8 * (i >> 2) + m0 + (i & 3)) * 33 + ln] = round_bfloat(acc[i], a.bfloat, kRoundNearest, 1);
+        wave_lds_sync();
+        const int row = lane >> 1, sub = lane & 1, r = r0 + row;
+        float xv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) xv[j] = ot[row * 33 + 16 * sub + j];
+        RowsPrepArgs ro{};
+        ro.codes = a.xo_codes; ro.sT = a.xo_exps;
+        ro.dpad = a.H * D; ro.nb = a.H * nbd; ro.D = a.H * D;
+        ro.op_kind = MXA_OP_MXINT8; ro.flush = a.flush_p; ro.bfloat = a.bfloat; ro.dt = kF32;
+        const int64_t orow = (int64_t)b_ * a.N + (r < r_end ? r : r0);
+        const int blk = h_ * nbd + dt / 32, c0 = h_ * D + dt + 16 * sub;
+        if (rows_prep_plain(ro)) rows_prep_block_plain<16, kF32>(ro, orow, blk, sub, c0, xv, r < r_end);
+        else rows_prep_block<16>(ro, orow, blk, sub, c0, xv, r < r_end);
+        wave_lds_sync();
+        continue;
       }
       // ---- 3. output rows (128-B segments per row) --------------------------------
       if (dt + ln < D) {

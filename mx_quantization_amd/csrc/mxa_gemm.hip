@@ -1,0 +1,108 @@
+// Launches of the block-scaled MX GEMM (mxa_gemm.hpp) and the mx.Linear entry point of
+// include/mxa.h (mxa_linear: x -> MX codes along in_features -> GEMM with a prepared weight).
+#include <algorithm>
+
+#include "mxa_gemm.hpp"
+#include "mxa_launch.hpp"
+
+namespace mxa {
+
+// shifted int32 block sums stay exact while nbk * 32 * 127^2 * 2^smax < 2^31
+int gemm_smax(int nbk) {
+  int s = -1;
+  while ((int64_t)nbk * 516128 * ((int64_t)1 << (s + 1)) < ((int64_t)1 << 31)) ++s;
+  return s;
+}
+
+int64_t gemm_slow_bytes(int M, int Nc, int64_t batch) {
+  const int64_t tiles = (int64_t)((M + kGemmRows - 1) / kGemmRows) * ((Nc + kGemmCols - 1) / kGemmCols) * batch;
+  return (4 * (1 + 4 * tiles) + 255) / 256 * 256;
+}
+
+// slow: gemm_slow_bytes of device scratch (the fp64 kernel's list)
+int launch_gemm(const GemmArgs& ga0, int64_t batch, int* slow, hipStream_t stream) {
+  GemmArgs ga = ga0;
+  if (ga.M <= 0 || ga.Nc <= 0 || ga.nbk <= 0 || batch <= 0 || !slow) return MXA_ERR_ARG;
+  ga.smax = gemm_smax(ga.nbk);
+  const size_t lds = gemm_lds(ga.nbk).total;
+  const int64_t gx = (ga.Nc + kGemmCols - 1) / kGemmCols, gy = (ga.M + kGemmRows - 1) / kGemmRows;
+  if (lds > 160 * 1024 || gy > 65535 || gx * gy * batch * 4 >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;
+  for (const void* k : {reinterpret_cast<const void*>(&mx_gemm_kernel), reinterpret_cast<const void*>(&mx_gemm_slow_kernel)})
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
+  if (hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
+  ga.slow = slow;
+  // grid.z <= 65535: larger batches in slices (each slice lists its slow waves by its own
+  // batch index, so every slice runs its own fp64 pass)
+  const int64_t esz = (ga.linear || ga.dt == kF32) ? 4 : 2;
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    GemmArgs gs = ga;
+    gs.a += b0 * ga.a_bat; gs.ae += b0 * ga.ae_bat; gs.b += b0 * ga.b_bat; gs.be += b0 * ga.be_bat;
+    gs.c = static_cast<unsigned char*>(ga.c) + b0 * ga.c_bat * esz;
+    const int64_t nb = std::min<int64_t>(65535, batch - b0);
+    if (b0 > 0 && hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
+    hipLaunchKernelGGL(mx_gemm_kernel, dim3((unsigned)gx, (unsigned)gy, (unsigned)nb), dim3(256), lds, stream, gs);
+    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+    const unsigned sgrid = (unsigned)std::min<int64_t>(gx * gy * nb * 4, 1024);
+    hipLaunchKernelGGL(mx_gemm_slow_kernel, dim3(sgrid), dim3(256), lds, stream, gs);
+    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  }
+  return MXA_OK;
+}
+
+// GEMM of MX rows (rows_prep layout: codes [rows][Cpad], exponents [rows][nbk]) with a
+// prepared Linear weight (its row-major codes / exponents): out = mx.Linear epilogue
+int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int in_f, const void* wq, int out_f,
+                        const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast, int* slow,
+                        hipStream_t stream) {
+  const LinearLayout W = linear_layout(out_f, in_f, out_f);  // raw regions do not depend on gw
+  const unsigned char* wb = static_cast<const unsigned char*>(wq);
+  GemmArgs g{};
+  g.a = xc; g.ae = xs; g.lda = W.Cpad;
+  g.b = reinterpret_cast<const int8_t*>(wb + W.rawc); g.ldb = W.Cpad;
+  g.be = reinterpret_cast<const int16_t*>(wb + W.rawe); g.be_n = W.nbk; g.be_k = 1;
+  g.M = (int)rows; g.Nc = out_f; g.nbk = W.nbk;
+  g.linear = 1; g.dt = kF32; g.bfloat = bfloat; g.autocast = autocast; g.bias = bias;
+  g.c = out; g.ldc = out_row_stride;
+  if (rows > ((int64_t)1 << 31) - 1) return MXA_ERR_UNSUPPORTED;
+  return launch_gemm(g, 1, slow, stream);
+}
+
+}  // namespace mxa
+
+using namespace mxa;
+
+extern "C" int64_t mxa_linear_workspace_bytes(int64_t rows, int32_t in_features, int32_t out_features) {
+  if (rows <= 0 || in_features <= 0 || out_features <= 0 || rows > INT32_MAX) return -1;
+  const int64_t nbk = (in_features + 31) / 32;
+  return (rows * nbk * 32 + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256 +
+         gemm_slow_bytes((int)rows, out_features, 1);
+}
+
+extern "C" int mxa_linear(const float* x, int64_t rows, int32_t in_features, int64_t x_row_stride, const void* wq,
+                          int32_t out_features, const float* bias, float* out, int64_t out_row_stride,
+                          int32_t flush_subnormals, int32_t bfloat, int32_t autocast_dtype, void* workspace,
+                          int64_t workspace_bytes, hipStream_t stream) {
+  if (!x || !wq || !out || rows <= 0 || in_features <= 0 || out_features <= 0 || x_row_stride < in_features ||
+      out_row_stride < out_features)
+    return MXA_ERR_ARG;
+  if (bfloat != 0 && bfloat != 32 && (bfloat < 10 || bfloat > 31)) return MXA_ERR_ARG;
+  if (autocast_dtype != 0 && autocast_dtype != MXA_DT_F16 && autocast_dtype != MXA_DT_BF16) return MXA_ERR_ARG;
+  if (!linear_weight_verify_any_group(wq, out_features, in_features, flush_subnormals, bfloat, stream))
+    return MXA_ERR_ARG;
+  const int64_t need = mxa_linear_workspace_bytes(rows, in_features, out_features);
+  if (!workspace || workspace_bytes < need || !aligned16(workspace)) return MXA_ERR_WORKSPACE;
+  const int nbk = (in_features + 31) / 32, Cpad = 32 * nbk;
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  RowsPrepArgs rx{};
+  rx.x = x; rx.s0 = 0; rx.s1 = 0; rx.s2 = x_row_stride;
+  rx.H = 1; rx.R = rows; rx.rows = rows; rx.D = in_features; rx.nb = nbk; rx.dpad = Cpad;
+  rx.vec4 = aligned16(x) && x_row_stride % 4 == 0;
+  rx.op_kind = MXA_OP_MXINT8; rx.flush = flush_subnormals; rx.bfloat = bfloat; rx.dt = MXA_DT_F32;
+  rx.codes = reinterpret_cast<int8_t*>(ws);
+  rx.sT = reinterpret_cast<int16_t*>(ws + (rows * Cpad + 255) / 256 * 256);
+  int rc = launch_rows_prep(rx, stream);
+  if (rc) return rc;
+  int* slow = reinterpret_cast<int*>(ws + (rows * Cpad + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256);
+  return launch_linear_codes(rx.codes, rx.sT, rows, in_features, wq, out_features, bias, out, out_row_stride, bfloat,
+                             autocast_dtype, slow, stream);
+}

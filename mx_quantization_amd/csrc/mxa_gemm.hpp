@@ -1,0 +1,276 @@
+// Block-scaled MX GEMM on int8 MFMA: C[b] = MX(A[b], along K) @ MX(B[b], along K)^T,
+// each product rounded once from its exact value.
+//
+// Serves the two plain GEMMs around the attention core that the patched modules run
+// through the reference's mx ops:
+//   mx.matmul   microxscaling/mx/matmul.py:31-100 (the drop-in's QK^T and P.V,
+//               workloads/deit/scripts/main.py:101, :152)
+//   mx.Linear   microxscaling/mx/linear.py:20-103 (the proj Linear behind the attention,
+//               deit main.py:154, DiT models.py:227; the drop-in's every Linear)
+// Operands are what the prep kernels write: codes int8 row-major along K (A: [M][lda],
+// B^T: [Nc][ldb]) and a code unit's exponent per 32-element block (value = code * 2^e,
+// -32768 = a NaN block).
+//
+// Workgroup: 64 rows x 128 columns, four waves of 32 rows x 64 columns -- two
+// independent 32x32 accumulator chains per wave sharing the A operand.  Operands go
+// straight from global memory into the MFMA registers (the lane maps of
+// v_mfma_i32_32x32x32_i8 read 16 contiguous bytes of one row: no LDS staging), loaded two
+// K-blocks ahead.  K = 32 = one MX block per MFMA, so every block keeps its exact int32
+// sum; the block's scale 2^(ea + eb) is applied as a shift of that sum relative to the
+// row's and the column's smallest block exponent (exponent offsets staged in LDS), and the
+// int32 total converts once: the correctly rounded exact product.  A wave whose rows' and
+// columns' exponent spreads could overflow int32 (or whose result could be subnormal)
+// sums the blocks in fp64 instead (exact while they span <= 34 bits, within fp32 rounding
+// beyond; the reference's own fp32 GEMM order is unpinned).  The MFMA of
+// block j + 1 is issued before the epilogue of block j.
+#pragma once
+#include "mxa_proj_args.hpp"
+
+namespace mxa {
+
+constexpr int kGemmRows = 64, kGemmCols = 128;
+
+struct GemmLds {
+  size_t xe, ce, rlo, rn, clo, cn, total;
+};
+__host__ __device__ inline GemmLds gemm_lds(int nbk) {
+  GemmLds L;
+  size_t o = 0;
+  L.xe = o;  // row exponent offsets [nbk][64] int16
+  o += (size_t)nbk * kGemmRows * 2;
+  L.ce = o;  // column exponent offsets [nbk][128] int16
+  o += (size_t)nbk * kGemmCols * 2;
+  o = (o + 15) & ~(size_t)15;
+  L.rlo = o;
+  o += kGemmRows * 4;
+  L.rn = o;
+  o += kGemmRows * 4;
+  L.clo = o;
+  o += kGemmCols * 4;
+  L.cn = o;
+  o += kGemmCols * 4;
+  L.total = o;
+  return L;
+}
+
+// SLOW = false: the shifted-int32 path; a wave that fails its test appends its tile to
+// a.slow (count, then entries) and leaves.  SLOW = true: a fixed grid strides over that
+// list and sums those waves' blocks in fp64 (an empty list costs one read per workgroup).
+template <bool SLOW>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm, int tn, int only_wave,
+                                          unsigned char* smem) {
+  typedef int v16i_g __attribute__((ext_vector_type(16)));
+  typedef int v4i_g __attribute__((ext_vector_type(4)));
+  const int nbk = a.nbk;
+  const GemmLds L = gemm_lds(nbk);
+  int16_t* xe = reinterpret_cast<int16_t*>(smem + L.xe);
+  int16_t* ce = reinterpret_cast<int16_t*>(smem + L.ce);
+  int* rlo = reinterpret_cast<int*>(smem + L.rlo);
+  int* rn = reinterpret_cast<int*>(smem + L.rn);
+  int* clo = reinterpret_cast<int*>(smem + L.clo);
+  int* cn = reinterpret_cast<int*>(smem + L.cn);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m0g = tm * kGemmRows, n0g = tn * kGemmCols;
+  const int16_t* aeb = a.ae + bat * a.ae_bat;
+  const int16_t* beb = a.be + bat * a.be_bat;
+
+  // ---- per row / column of the tile: smallest finite block exponent, spread, NaN ----
+  // (rows / columns beyond the matrix: exponents 0, never NaN -- their results are dropped)
+  if (tid < kGemmRows + kGemmCols) {
+    const bool isrow = tid < kGemmRows;
+    const int i = isrow ? tid : tid - kGemmRows;
+    const bool valid = isrow ? m0g + i < a.M : n0g + i < a.Nc;
+    int lo = 1 << 20, hi = -(1 << 20), nan = 0;
+    if (valid) {
+      for (int kb = 0; kb < nbk; ++kb) {
+        const int e = exp_from16(isrow ? aeb[(int64_t)(m0g + i) * nbk + kb] : beb[(int64_t)(n0g + i) * a.be_n + kb * a.be_k]);
+        if (e == kExpNaN) {
+          nan = 1;
+        } else {
+          lo = min(lo, e);
+          hi = max(hi, e);
+        }
+      }
+    }
+    if (lo > hi) lo = hi = 0;
+    (isrow ? rlo : clo)[i] = lo;
+    (isrow ? rn : cn)[i] = nan;
+  }
+  __syncthreads();
+  for (int i = tid; i < nbk * kGemmRows; i += 256) {
+    const int kb = i / kGemmRows, r = i - kb * kGemmRows;
+    int e = m0g + r < a.M ? exp_from16(aeb[(int64_t)(m0g + r) * nbk + kb]) : 0;
+    xe[i] = (int16_t)(e == kExpNaN ? 0 : e - rlo[r]);
+  }
+  for (int i = tid; i < nbk * kGemmCols; i += 256) {
+    const int kb = i / kGemmCols, c = i - kb * kGemmCols;
+    int e = n0g + c < a.Nc ? exp_from16(beb[(int64_t)(n0g + c) * a.be_n + kb * a.be_k]) : 0;
+    ce[i] = (int16_t)(e == kExpNaN ? 0 : e - clo[c]);
+  }
+  __syncthreads();
+
+  // ---- this wave: rows wr0 .. +31, columns wc0 .. +63 of the tile ------------------
+  const int wr0 = 32 * (wave & 1), wc0 = 64 * (wave >> 1);
+  const int ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
+  // the wave's fast-path test: its rows' largest spread + its columns' largest spread,
+  // and the smallest output scale (a subnormal result would round twice)
+  auto wmax = [](int v) {
+    return (int)wave_reduce((uint32_t)(v + (1 << 20)), [](uint32_t x, uint32_t y) { return x > y ? x : y; }) - (1 << 20);
+  };
+  auto wmin = [](int v) {
+    return (int)wave_reduce((uint32_t)(v + (1 << 20)), [](uint32_t x, uint32_t y) { return x < y ? x : y; }) - (1 << 20);
+  };
+  const int rr = wr0 + ln, cc = wc0 + lane;
+  const bool rv = m0g + rr < a.M, cv = n0g + cc < a.Nc;
+  // spreads recomputed from the LDS offsets (row rr: lanes 0..31 and 32..63 alike)
+  int rsp = 0, csp = 0;
+  for (int kb = 0; kb < nbk; ++kb) {
+    rsp = max(rsp, (int)xe[kb * kGemmRows + rr]);
+    csp = max(csp, (int)ce[kb * kGemmCols + cc]);
+  }
+  const int srow = wmax(rv ? rsp : 0), scol = wmax(cv ? csp : 0);
+  const int lrow = wmin(rv ? rlo[rr] : (1 << 19)), lcol = wmin(cv ? clo[cc] : (1 << 19));
+  const bool fast = srow + scol <= a.smax && lrow + lcol >= -126;
+  if constexpr (!SLOW) {
+    if (!fast) {
+      if (lane == 0) {
+        const int64_t ntm = (a.M + kGemmRows - 1) / kGemmRows, ntn = (a.Nc + kGemmCols - 1) / kGemmCols;
+        a.slow[1 + atomicAdd(a.slow, 1)] = (int)(((bat * ntm + tm) * ntn + tn) * 4 + wave);
+      }
+      return;
+    }
+  } else {
+    if (wave != only_wave) return;
+  }
+
+  const int arow = min(m0g + wr0 + ln, a.M - 1);
+  const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
+  const int8_t* ap = a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
+  const int8_t* bp0 = a.b + bat * a.b_bat + (int64_t)bc0 * a.ldb + kh;
+  const int8_t* bp1 = a.b + bat * a.b_bat + (int64_t)bc1 * a.ldb + kh;
+  auto ld = [](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + 32 * kb); };
+  const v16i_g zero = {};
+  const int last = nbk - 1;
+  const int16_t* xrow = xe + wr0 + m0;
+  const int16_t* xcol = ce + wc0 + ln;
+
+  // output of chain j (columns wc0 + 32 j ..): value of element i of the lane
+  auto store = [&](int j, int i, float o) {
+    const int m = m0g + wr0 + 8 * (i >> 2) + m0 + (i & 3);
+    const int n = n0g + wc0 + 32 * j + ln;
+    if (m >= a.M || n >= a.Nc) return;
+    const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3), lc = wc0 + 32 * j + ln;
+    if (rn[lr] || cn[lc]) o = __uint_as_float(0x7FC00000u);
+    const int64_t off = bat * a.c_bat + (int64_t)m * a.ldc + n;
+    if (a.linear) {
+      o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+      o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
+      if (a.bias) o = round_bfloat(o + round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1), a.bfloat, kRoundNearest, 1);
+      static_cast<float*>(a.c)[off] = o;
+    } else {
+      store_dt(a.c, off, round_bfloat(round_dt(o, a.dt), a.bfloat, kRoundNearest, 1, a.dt), a.dt);
+    }
+  };
+
+  if constexpr (!SLOW) {
+    int acc0[16], acc1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0;
+    // block kb's shifted sums: row offset (4 rows per uint2 read) + column offset
+    auto epi = [&](const v16i_g& c0, const v16i_g& c1, int kb) {
+      const int d0 = xcol[kb * kGemmCols], d1 = xcol[kb * kGemmCols + 32];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint2 e4 = *reinterpret_cast<const uint2*>(xrow + kb * kGemmRows + 8 * q);
+        const int dx[4] = {(int)(int16_t)(e4.x & 0xFFFFu), (int)(int16_t)(e4.x >> 16), (int)(int16_t)(e4.y & 0xFFFFu),
+                           (int)(int16_t)(e4.y >> 16)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc0[4 * q + r] += (int)((uint32_t)c0[4 * q + r] << (dx[r] + d0));
+          acc1[4 * q + r] += (int)((uint32_t)c1[4 * q + r] << (dx[r] + d1));
+        }
+      }
+    };
+    // operand slots: E = even blocks, O = odd blocks, each loaded two blocks ahead
+    v4i_g aE = ld(ap, 0), bE0 = ld(bp0, 0), bE1 = ld(bp1, 0);
+    v4i_g aO = ld(ap, min(1, last)), bO0 = ld(bp0, min(1, last)), bO1 = ld(bp1, min(1, last));
+    v16i_g cA0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE0, zero, 0, 0, 0);
+    v16i_g cA1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE1, zero, 0, 0, 0);
+    v16i_g cB0, cB1;
+    aE = ld(ap, min(2, last)); bE0 = ld(bp0, min(2, last)); bE1 = ld(bp1, min(2, last));
+    for (int kb = 0;; kb += 2) {
+      // cA holds block kb
+      const bool h1 = kb + 1 < nbk;
+      if (h1) {
+        cB0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aO, bO0, zero, 0, 0, 0);
+        cB1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aO, bO1, zero, 0, 0, 0);
+        const int kn = min(kb + 3, last);
+        aO = ld(ap, kn); bO0 = ld(bp0, kn); bO1 = ld(bp1, kn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      epi(cA0, cA1, kb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!h1) break;
+      const bool h2 = kb + 2 < nbk;
+      if (h2) {
+        cA0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE0, zero, 0, 0, 0);
+        cA1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE1, zero, 0, 0, 0);
+        const int kn = min(kb + 4, last);
+        aE = ld(ap, kn); bE0 = ld(bp0, kn); bE1 = ld(bp1, kn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      epi(cB0, cB1, kb + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!h2) break;
+    }
+    const int lc0 = clo[wc0 + ln], lc1 = clo[wc0 + 32 + ln];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int lr = rlo[wr0 + 8 * (i >> 2) + m0 + (i & 3)];
+      store(0, i, ldexpf((float)acc0[i], lr + lc0));
+      store(1, i, ldexpf((float)acc1[i], lr + lc1));
+    }
+  } else {
+    // fp64 block sums, one chain at a time (registers for one double accumulator set)
+    for (int j = 0; j < 2; ++j) {
+      const int8_t* bp = j ? bp1 : bp0;
+      const int lc = clo[wc0 + 32 * j + ln];
+      double acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+      for (int kb = 0; kb < nbk; ++kb) {
+        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ld(bp, kb), zero, 0, 0, 0);
+        const int dc = xcol[kb * kGemmCols + 32 * j] + lc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3);
+          acc[i] += ldexp((double)c[i], xe[kb * kGemmRows + lr] + rlo[lr] + dc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) store(j, i, (float)acc[i]);
+    }
+  }
+}
+
+// (3 waves per SIMD: 166 VGPRs without spills; a cap of 4 spills ~640 registers)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void mx_gemm_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemm_tile<false>(a, blockIdx.z, blockIdx.y, blockIdx.x, -1, smem);
+}
+
+__global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = __builtin_amdgcn_readfirstlane(*a.slow);
+  const int64_t ntm = (a.M + kGemmRows - 1) / kGemmRows, ntn = (a.Nc + kGemmCols - 1) / kGemmCols;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t e = __builtin_amdgcn_readfirstlane(a.slow[1 + i]);
+    const int w = (int)(e & 3);
+    const int64_t t = e >> 2;
+    const int tn = (int)(t % ntn), tm = (int)((t / ntn) % ntm);
+    gemm_tile<true>(a, t / (ntn * ntm), tm, tn, w, smem);
+    __syncthreads();  // the next entry restages the exponent tables
+  }
+}
+
+}  // namespace mxa

@@ -160,6 +160,8 @@ __global__ void linear_header_kernel(LinearWeightHeader* h, LinearWeightHeader v
   if (threadIdx.x == 0) *h = v;
 }
 
+LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat);
+
 // prepared buffers whose header is known to the host (pointer -> header)
 static std::mutex g_wmu;
 static std::unordered_map<const void*, LinearWeightHeader> g_weights;
@@ -184,6 +186,26 @@ bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStr
   if (!(h == want)) return false;
   linear_weight_note(wq, h);
   return true;
+}
+
+bool linear_weight_verify_any_group(const void* wq, int out_f, int in_f, int flush, int bfloat, hipStream_t stream) {
+  LinearWeightHeader h{};
+  bool known = false;
+  {
+    std::lock_guard<std::mutex> g(g_wmu);
+    auto it = g_weights.find(wq);
+    if (it != g_weights.end()) h = it->second, known = true;
+  }
+  if (!known) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    if (hipMemcpyAsync(&h, wq, sizeof(h), hipMemcpyDeviceToHost, stream) != hipSuccess) return false;
+    if (hipStreamSynchronize(stream) != hipSuccess) return false;
+    if (h.magic != kLinearWeightMagic || h.gw <= 0 || h.out_f % h.gw) return false;
+    linear_weight_note(wq, h);
+  }
+  LinearWeightHeader want = linear_weight_header(out_f, in_f, h.gw, flush, bfloat);
+  return h == want;
 }
 
 LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat) {

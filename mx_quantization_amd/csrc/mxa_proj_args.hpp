@@ -75,4 +75,21 @@ struct ProjArgs {
   ColsPrepArgs cv;      // V outputs (cols_prep layout)
 };
 
+// block-scaled MX GEMM (mxa_gemm.hpp): mx.matmul and mx.Linear
+struct GemmArgs {
+  const int8_t* a;   // A codes: (bat, m, k) at bat * a_bat + m * lda + k
+  const int16_t* ae; // A exponents: (bat, m, kb) at bat * ae_bat + m * nbk + kb
+  const int8_t* b;   // B^T codes: (bat, n, k) at bat * b_bat + n * ldb + k
+  const int16_t* be; // B exponents: (bat, n, kb) at bat * be_bat + n * be_n + kb * be_k
+  int64_t a_bat, ae_bat, b_bat, be_bat, be_n, be_k, lda, ldb;
+  int M, Nc, nbk;
+  int smax;           // largest row + column spread whose shifted int32 sums cannot overflow
+  int linear;         // epilogue: 0 mx.matmul (store in dt), 1 mx.Linear (fp32, bias)
+  int dt, bfloat, autocast;
+  const float* bias;  // linear: [Nc] or null
+  void* c;            // (bat, m, n) at bat * c_bat + m * ldc + n
+  int64_t c_bat, ldc;
+  int* slow;  // waves for the fp64 kernel: count, then (tile * 4 + wave); zeroed before the launch
+};
+
 }  // namespace mxa

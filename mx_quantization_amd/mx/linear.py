@@ -1,11 +1,12 @@
 """MX Linear -- drop-in for microxscaling/mx/linear.py (forward / inference).
 
 out = MX(x, along in_features) @ MX(W, along in_features)^T (+ bias), on the
-device through mxa_matmul.  This is the qkv / proj projection around the
-attention core (a SURVEY §8f "next" row): the unfused drop-in, so the patched
-modules' `from mx import Linear` keeps working.  The fused forms are
-mx_quantization_amd.mx_qkv_attention (qkv Linear -> attention operands) and the
-proj Linear on the attention output (include/mxa.h)."""
+device: float32 inputs through mxa_linear (the block-scaled int8-MFMA GEMM with the
+weight prepared once per weight version), other dtypes through mxa_matmul.  This is the
+qkv / proj projection around the attention core (a SURVEY §8f "next" row) as the
+patched modules' `from mx import Linear` sees it.  The fused forms are
+mx_quantization_amd.mx_qkv_attention (qkv Linear -> attention operands, and with
+proj_weight the proj Linear behind it: include/mxa.h mxa_attention_proj)."""
 from __future__ import annotations
 
 import torch
@@ -16,12 +17,35 @@ from .matmul import _check_specs, _mbits
 from .specs import apply_mx_specs, mx_assert_test
 
 
+_PREPARED = {}  # (weight storage, version, flush, bfloat) -> LinearWeightMX
+
+
+def _prepared_weight(weight, s):
+    """The weight's MX codes, prepared once per weight version (inference: constant)."""
+    key = (weight.data_ptr(), tuple(weight.shape), weight._version, bool(s["mx_flush_fp32_subnorms"]), int(s["bfloat"]))
+    wq = _PREPARED.get(key)
+    if wq is None:
+        if len(_PREPARED) > 256:
+            _PREPARED.clear()
+        wq = ops.LinearWeightMX(weight.detach().contiguous(), weight.shape[0], s["mx_flush_fp32_subnorms"], s["bfloat"])
+        _PREPARED[key] = wq
+    return wq
+
+
 def linear(input, weight, bias=None, mx_specs=None, prequantized_weights=False, name=None):
     """LinearFunction.forward (linear.py:20-103)."""
     if mx_specs is None:
         return torch.nn.functional.linear(input, weight, bias)
     s = apply_mx_specs(mx_specs)
     _check_specs(s)
+    if (input.dtype == torch.float32 and weight.dtype == torch.float32 and not prequantized_weights
+            and _mbits(s["a_elem_format"]) == 8 and _mbits(s["w_elem_format"]) == 8
+            and (bias is None or bias.dtype == torch.float32)
+            and all(s.get(r, "nearest") == "nearest" for r in ("round_output", "round_weight", "round_mx_output"))):
+        # mxa_linear: bf(x), MX along in_features, exact-then-rounded product, bf(out + bf(bias))
+        wq = _prepared_weight(weight, s)
+        return ops.mx_linear(input, wq, bias, flush_subnormals=s["mx_flush_fp32_subnorms"], bfloat=s["bfloat"],
+                             autocast=ops.autocast_dtype(input.device.type))
     bf_in = quantize_elemwise_op(input, mx_specs=s, round=s["round_output"])
     bf_w = weight if prequantized_weights else quantize_elemwise_op(weight, mx_specs=s, round=s["round_weight"])
     x2 = bf_in.reshape(1, -1, bf_in.shape[-1])

@@ -373,10 +373,93 @@ class LinearWeightMX:
         self.flush, self.bfloat = bool(flush_subnormals), int(bfloat)
 
 
+def _prepared(weight, group_width: int, flush_subnormals: bool, bfloat: int) -> "LinearWeightMX":
+    wq = weight if isinstance(weight, LinearWeightMX) else LinearWeightMX(weight, group_width, flush_subnormals, bfloat)
+    if (wq.flush, wq.bfloat) != (bool(flush_subnormals), int(bfloat)):
+        raise ValueError("the prepared weight was quantized with other flush / bfloat settings")
+    return wq
+
+
+def mx_linear(x: torch.Tensor, weight, bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False,
+              bfloat: int = 0, autocast: Optional[torch.dtype] = None) -> torch.Tensor:
+    """mx.Linear forward (microxscaling/mx/linear.py:20-103; include/mxa.h mxa_linear):
+    x (..., in_features) float32, weight an (out, in) tensor or a LinearWeightMX (any group
+    width); out (..., out) float32 = bf(fl32(MX(x) @ MX(W)^T)) [+ bf(bias)], every product
+    the exact sum rounded once.  autocast: the product rounded to float16 / bfloat16 before
+    the fp32 bias add (F.linear under torch.autocast)."""
+    dev = require_device(x, bias)
+    x = _f32(x, "x")
+    wq = _prepared(weight, weight.shape[0] if not isinstance(weight, LinearWeightMX) else 1, flush_subnormals, bfloat)
+    if x.shape[-1] != wq.in_features:
+        raise ValueError(f"x has {x.shape[-1]} features, the weight {wq.in_features}")
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    rows = x2.shape[0]
+    out = torch.empty((rows, wq.out_features), dtype=torch.float32, device=dev)
+    if rows == 0:
+        return out.reshape(x.shape[:-1] + (wq.out_features,))
+    ac = 0
+    if autocast is not None and autocast != torch.float32:
+        ac = N.DTYPES[autocast]
+    bptr = None
+    if bias is not None:
+        bias = _f32(bias, "bias").contiguous()
+        bptr = bias.data_ptr()
+    nbytes = lib().mxa_linear_workspace_bytes(rows, wq.in_features, wq.out_features)
+    ws = _workspace(dev, nbytes)
+    check(lib().mxa_linear(x2.data_ptr(), rows, wq.in_features, x2.stride(0), wq.buf.data_ptr(), wq.out_features,
+                           bptr, out.data_ptr(), out.stride(0), int(bool(flush_subnormals)), int(bfloat), ac,
+                           ws.data_ptr(), ws.numel(), stream_ptr(dev)), "mxa_linear")
+    return out.reshape(x.shape[:-1] + (wq.out_features,))
+
+
+def _proj_params(proj_weight, proj_bias, C: int, rows: int, flush_subnormals: bool, bfloat: int, dev):
+    """(ProjParams, y (rows, out_features), keep) for the proj Linear behind the attention."""
+    wp = _prepared(proj_weight, proj_weight.shape[0] if not isinstance(proj_weight, LinearWeightMX) else 1,
+                   flush_subnormals, bfloat)
+    if wp.in_features != C:
+        raise ValueError(f"proj weight takes {wp.in_features} features, the attention gives H*D = {C}")
+    pj = N.ProjParams()
+    pj.wq, pj.out_features = wp.buf.data_ptr(), wp.out_features
+    keep = [wp]
+    if proj_bias is not None:
+        pb = _f32(proj_bias, "proj_bias").contiguous()
+        keep.append(pb)
+        pj.bias = pb.data_ptr()
+    y = torch.empty((rows, wp.out_features), dtype=torch.float32, device=dev)
+    pj.y, pj.y_row_stride = y.data_ptr(), y.stride(0)
+    return pj, y, keep
+
+
+def mx_topk_attention_proj(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, proj_weight,
+                           proj_bias: Optional[torch.Tensor] = None, k_top: int = 20, pred_mode: str = "ex_pred",
+                           approx: bool = True, bias: Optional[torch.Tensor] = None, flush_subnormals: bool = False,
+                           bfloat: int = 0, elsa_proj: Optional[torch.Tensor] = None):
+    """The top-k attention core with the proj mx.Linear fused behind it (include/mxa.h
+    mxa_attention_proj): y = proj(out.transpose(1, 2).reshape(B, N, H*D)) as (B, N, out)
+    float32, plus idx (B,H,N,k).  float32 q, k, v (views fine)."""
+    p, dev, (B, H, Nq, T, D), keep = _attn_params(q, k, v, scale, k_top, pred_mode, True, approx, bias,
+                                                  flush_subnormals, bfloat, elsa_proj)
+    if p.dtype != N.DT_F32:
+        raise TypeError("the fused proj takes float32 q, k, v")
+    idx = torch.empty((B, H, Nq, k_top), dtype=torch.int64, device=dev)
+    p.idx_out = idx.data_ptr()
+    pj, y, keep2 = _proj_params(proj_weight, proj_bias, H * D, B * Nq, flush_subnormals, bfloat, dev)
+    nbytes = lib().mxa_attention_proj_workspace_bytes(ctypes.byref(p), None, ctypes.byref(pj))
+    if nbytes < 0:
+        raise ValueError("bad attention shape")
+    ws = _workspace(dev, nbytes)
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    check(lib().mxa_attention_proj(ctypes.byref(p), None, ctypes.byref(pj), stream_ptr(dev)), "mxa_attention_proj")
+    return y.reshape(B, Nq, -1), idx
+
+
 def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_heads: int, scale: float,
                      k_top: int = 20, pred_mode: str = "ex_pred", top_k: bool = True, approx: bool = True,
                      flush_subnormals: bool = False, bfloat: int = 0, return_qkv: bool = False,
-                     elsa_proj: Optional[torch.Tensor] = None, autocast: Optional[torch.dtype] = None):
+                     elsa_proj: Optional[torch.Tensor] = None, autocast: Optional[torch.dtype] = None,
+                     proj_weight=None, proj_bias: Optional[torch.Tensor] = None):
     """The qkv mx.Linear fused into the attention core (include/mxa.h mxa_qkv_attention):
     x (B, N, C) float32 tokens; weight a (3C', C) tensor or a LinearWeightMX; returns
     (out (B,H,N,D), idx (B,H,N,k) or None[, qkv (B,N,3C') fp32 projection]).
@@ -422,6 +505,21 @@ def mx_qkv_attention(x: torch.Tensor, weight, bias: Optional[torch.Tensor], num_
         xp.bias = bias.data_ptr()
     qkv = torch.empty((B, Ntok, wq.out_features), dtype=torch.float32, device=dev) if return_qkv else None
     xp.qkv_out = qkv.data_ptr() if return_qkv else None
+    if proj_weight is not None:
+        # ... then the proj mx.Linear on the attention output (mxa_attention_proj): (y, idx[, qkv])
+        if not top_k or autocast not in (None, torch.float32):
+            raise ValueError("the fused proj runs on the float32 top-k path")
+        pj, y, keep2 = _proj_params(proj_weight, proj_bias, num_heads * D, B * Ntok, flush_subnormals, bfloat, dev)
+        p.out = None
+        nbytes = lib().mxa_attention_proj_workspace_bytes(ctypes.byref(p), ctypes.byref(xp), ctypes.byref(pj))
+        if nbytes < 0:
+            raise ValueError("bad shape")
+        ws = _workspace(dev, nbytes)
+        p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+        check(lib().mxa_attention_proj(ctypes.byref(p), ctypes.byref(xp), ctypes.byref(pj), stream_ptr(dev)),
+              "mxa_attention_proj")
+        y = y.reshape(B, Ntok, -1)
+        return (y, idx, qkv) if return_qkv else (y, idx)
     nbytes = lib().mxa_qkv_attention_workspace_bytes(ctypes.byref(p), ctypes.byref(xp))
     if nbytes < 0:
         raise ValueError("bad shape")

@@ -231,6 +231,48 @@ def gen_linear_qkv():
     print("wrote linear_qkv")
 
 
+def gen_linear_proj():
+    """linear_proj.npz: the reference's mx.Linear proj behind the attention (deit main.py:152-154,
+    DiT models.py:225-227): x -> qkv Linear -> ex_pred top-k attention -> transpose/reshape ->
+    proj Linear, at the DeiT-tiny block (3 heads of 64, k = 20) and a DiT-like block (4 heads of
+    72, N = 256, k = 154: a 32-element block of C spans two heads); plus the proj Linear alone
+    on given inputs (its exact-then-rounded product pinned bit for bit) and a ragged Linear
+    (rows / features not multiples of 32)."""
+    from mx import Linear
+    store = {}
+    for tag, (N, H, D, k_top, seed) in (("deit", (197, 3, 64, 20, 40)), ("dit", (256, 4, 72, 154, 50))):
+        C = H * D
+        x = torch.from_numpy(rnd((1, N, C), seed))
+        W = torch.from_numpy(rnd((3 * C, C), seed + 1, 0.08))
+        b = torch.from_numpy(rnd((3 * C,), seed + 2, 0.1))
+        Wp = torch.from_numpy(rnd((C, C), seed + 3, 0.08))
+        bp = torch.from_numpy(rnd((C,), seed + 4, 0.1))
+        qkv_l = Linear(C, 3 * C, bias=True, mx_specs=specs())
+        qkv_l.weight.data, qkv_l.bias.data = W.clone(), b.clone()
+        proj_l = Linear(C, C, bias=True, mx_specs=specs())
+        proj_l.weight.data, proj_l.bias.data = Wp.clone(), bp.clone()
+        sc = D ** -0.5
+        with torch.no_grad():
+            qkv = qkv_l(x)
+            q, k, v = qkv.reshape(1, N, 3, H, D).permute(2, 0, 3, 1, 4)
+            r = attention_glue(q.contiguous(), k.contiguous(), v.contiguous(), specs(), sc, k_top, "ex_pred")
+            xo = torch.from_numpy(r["out"]).transpose(1, 2).reshape(1, N, C)
+            y = proj_l(xo)
+        store.update({f"{tag}/x": x.numpy(), f"{tag}/W": W.numpy(), f"{tag}/b": b.numpy(), f"{tag}/Wp": Wp.numpy(),
+                      f"{tag}/bp": bp.numpy(), f"{tag}/scale": np.float32(sc), f"{tag}/H": np.int64(H),
+                      f"{tag}/k": np.int64(k_top), f"{tag}/idx": r["idx"], f"{tag}/attn_out": xo.numpy(),
+                      f"{tag}/y": y.numpy()})
+    xr = torch.from_numpy(rnd((37, 100), 60))
+    Wr = torch.from_numpy(rnd((70, 100), 61, 0.1))
+    br = torch.from_numpy(rnd((70,), 62, 0.1))
+    lr = Linear(100, 70, bias=True, mx_specs=specs())
+    lr.weight.data, lr.bias.data = Wr.clone(), br.clone()
+    with torch.no_grad():
+        store.update({"ragged/x": xr.numpy(), "ragged/W": Wr.numpy(), "ragged/b": br.numpy(), "ragged/y": lr(xr).numpy()})
+    np.savez_compressed(os.path.join(OUT, "linear_proj.npz"), **store)
+    print("wrote linear_proj")
+
+
 def gen_analysis():
     """analysis.npz: the reference's funcs/analysis.py hooks (total_chosen_k :56-110,
     diff_idx_analysis :136-157, save_idx_file :22-29) on seeded top-k outputs."""
@@ -506,7 +548,7 @@ def attention_glue_t(q, k, v, s, scale, k_top, mode, top_k=True):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv", "analysis",
+    which = sys.argv[1:] or ["quant_kat", "topk_ties", "attention", "attention_extra", "linear_qkv", "linear_proj", "analysis",
                              "dtype"]
     for w in which:
         globals()["gen_" + w]()

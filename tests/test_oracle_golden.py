@@ -239,3 +239,13 @@ def test_dtype_exponent_rule_matches_reference_on_every_value(dt):
     got = O.floor_log2_dtype(d[f"{dt}/sexp_x"], dt)
     ref = d[f"{dt}/sexp_none"].astype(np.float64)
     assert np.array_equal(got, ref)
+
+
+def test_oracle_linear_proj_golden():
+    """oracle.mx_linear against the reference's mx.Linear (linear_proj.npz): the proj on the
+    reference attention output at the DeiT-tiny / DiT-like widths and a ragged Linear."""
+    d = np.load(os.path.join(G, "linear_proj.npz"))
+    for tag in ("deit", "dit"):
+        y = O.mx_linear(d[f"{tag}/attn_out"], d[f"{tag}/Wp"], d[f"{tag}/bp"])
+        assert np.array_equal(y, d[f"{tag}/y"]), tag
+    assert np.array_equal(O.mx_linear(d["ragged/x"], d["ragged/W"], d["ragged/b"]), d["ragged/y"])
