@@ -20,16 +20,16 @@ int64_t gemm_slow_bytes(int M, int Nc, int64_t batch) {
 }
 
 // slow: gemm_slow_bytes of device scratch (the fp64 kernel's list)
-int launch_gemm(const GemmArgs& ga0, int64_t batch, int* slow, hipStream_t stream) {
+template <bool PLAIN>
+static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, int* slow, hipStream_t stream) {
   GemmArgs ga = ga0;
-  if (ga.M <= 0 || ga.Nc <= 0 || ga.nbk <= 0 || batch <= 0 || !slow) return MXA_ERR_ARG;
   ga.smax = gemm_smax(ga.nbk);
   const size_t lds = gemm_lds(ga.nbk).total;
   const int64_t gx = (ga.Nc + kGemmCols - 1) / kGemmCols, gy = (ga.M + kGemmRows - 1) / kGemmRows;
   if (lds > 160 * 1024 || gy > 65535 || gx * gy * batch * 4 >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;
-  for (const void* k : {reinterpret_cast<const void*>(&mx_gemm_kernel), reinterpret_cast<const void*>(&mx_gemm_slow_kernel)})
+  for (const void* k : {reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN>),
+                        reinterpret_cast<const void*>(&mx_gemm_slow_kernel<PLAIN>)})
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
-  if (hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
   ga.slow = slow;
   // grid.z <= 65535: larger batches in slices (each slice lists its slow waves by its own
   // batch index, so every slice runs its own fp64 pass)
@@ -39,14 +39,20 @@ int launch_gemm(const GemmArgs& ga0, int64_t batch, int* slow, hipStream_t strea
     gs.a += b0 * ga.a_bat; gs.ae += b0 * ga.ae_bat; gs.b += b0 * ga.b_bat; gs.be += b0 * ga.be_bat;
     gs.c = static_cast<unsigned char*>(ga.c) + b0 * ga.c_bat * esz;
     const int64_t nb = std::min<int64_t>(65535, batch - b0);
-    if (b0 > 0 && hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
-    hipLaunchKernelGGL(mx_gemm_kernel, dim3((unsigned)gx, (unsigned)gy, (unsigned)nb), dim3(256), lds, stream, gs);
+    if (hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
+    hipLaunchKernelGGL(mx_gemm_kernel<PLAIN>, dim3((unsigned)gx, (unsigned)gy, (unsigned)nb), dim3(256), lds, stream, gs);
     if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
     const unsigned sgrid = (unsigned)std::min<int64_t>(gx * gy * nb * 4, 1024);
-    hipLaunchKernelGGL(mx_gemm_slow_kernel, dim3(sgrid), dim3(256), lds, stream, gs);
+    hipLaunchKernelGGL(mx_gemm_slow_kernel<PLAIN>, dim3(sgrid), dim3(256), lds, stream, gs);
     if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   }
   return MXA_OK;
+}
+
+int launch_gemm(const GemmArgs& ga, int64_t batch, int* slow, hipStream_t stream) {
+  if (ga.M <= 0 || ga.Nc <= 0 || ga.nbk <= 0 || batch <= 0 || !slow) return MXA_ERR_ARG;
+  const bool plain = (ga.bfloat == 0 || ga.bfloat == 32) && (ga.linear ? ga.autocast == 0 : ga.dt == kF32);
+  return plain ? launch_gemm_p<true>(ga, batch, slow, stream) : launch_gemm_p<false>(ga, batch, slow, stream);
 }
 
 // GEMM of MX rows (rows_prep layout: codes [rows][Cpad], exponents [rows][nbk]) with a

@@ -56,7 +56,9 @@ __host__ __device__ inline GemmLds gemm_lds(int nbk) {
 // SLOW = false: the shifted-int32 path; a wave that fails its test appends its tile to
 // a.slow (count, then entries) and leaves.  SLOW = true: a fixed grid strides over that
 // list and sums those waves' blocks in fp64 (an empty list costs one read per workgroup).
-template <bool SLOW>
+// PLAIN: float32 output, no bfloat / autocast rounding (the bench and workload settings):
+// the epilogue is a store (+ bias), compiled without the general rounding code.
+template <bool SLOW, bool PLAIN>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm, int tn, int only_wave,
                                           unsigned char* smem) {
   typedef int v16i_g __attribute__((ext_vector_type(16)));
@@ -162,7 +164,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3), lc = wc0 + 32 * j + ln;
     if (rn[lr] || cn[lc]) o = __uint_as_float(0x7FC00000u);
     const int64_t off = bat * a.c_bat + (int64_t)m * a.ldc + n;
-    if (a.linear) {
+    if constexpr (PLAIN) {
+      static_cast<float*>(a.c)[off] = a.bias ? o + a.bias[n] : o;
+    } else if (a.linear) {
       o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
       o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
       if (a.bias) o = round_bfloat(o + round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1), a.bfloat, kRoundNearest, 1);
@@ -254,11 +258,13 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
 }
 
 // (3 waves per SIMD: 166 VGPRs without spills; a cap of 4 spills ~640 registers)
+template <bool PLAIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void mx_gemm_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemm_tile<false>(a, blockIdx.z, blockIdx.y, blockIdx.x, -1, smem);
+  gemm_tile<false, PLAIN>(a, blockIdx.z, blockIdx.y, blockIdx.x, -1, smem);
 }
 
+template <bool PLAIN>
 __global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = __builtin_amdgcn_readfirstlane(*a.slow);
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
     const int w = (int)(e & 3);
     const int64_t t = e >> 2;
     const int tn = (int)(t % ntn), tm = (int)((t / ntn) % ntm);
-    gemm_tile<true>(a, t / (ntn * ntm), tm, tn, w, smem);
+    gemm_tile<true, PLAIN>(a, t / (ntn * ntm), tm, tn, w, smem);
     __syncthreads();  // the next entry restages the exponent tables
   }
 }

@@ -45,6 +45,16 @@ for cfg in ${BENCH_CONFIGS:-deit_base dit_xl2 pixart_cross}; do
     python tools/hbm_traffic.py $O/pqf_$cfg $O/pqw_$cfg $O/${T}_traffic_qkv_$cfg.json || exit $?
     pmc pq1_$cfg qkv SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_I8 SQ_WAVE_CYCLES SQ_WAIT_ANY || exit $?
     python tools/pmc_summary.py "$O/pq1_$cfg/**/*counter_collection.csv" --json $O/${T}_pmc_qkv_$cfg.json > $O/${T}_pmc_qkv_$cfg.txt || exit $?
+    # x -> qkv Linear -> attention -> proj Linear (the GEMM kernel's own passes)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/profp_$cfg -o run --output-format csv -- \
+      python bench.py --config $cfg --steps 6 --warmup 2 --no-cpu-baseline --no-parity --lines qkvproj \
+      > $O/profp_bench_$cfg.json 2> $O/profp_$cfg.err || exit $?
+    find $O/profp_$cfg -name "*kernel_stats.csv" -exec cp {} $O/${T}_rocprof_qkvproj_$cfg.csv \;
+    pmc ppf_$cfg qkvproj FETCH_SIZE || exit $?
+    pmc ppw_$cfg qkvproj WRITE_SIZE || exit $?
+    python tools/hbm_traffic.py $O/ppf_$cfg $O/ppw_$cfg $O/${T}_traffic_qkvproj_$cfg.json || exit $?
+    pmc pp1_$cfg qkvproj SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_I8 SQ_WAVE_CYCLES SQ_WAIT_ANY || exit $?
+    python tools/pmc_summary.py "$O/pp1_$cfg/**/*counter_collection.csv" --json $O/${T}_pmc_qkvproj_$cfg.json > $O/${T}_pmc_qkvproj_$cfg.txt || exit $?
   fi
   timeout -k 10 300 python bench.py --config $cfg --traffic-json $O/${T}_traffic_$cfg.json --pmc-json $O/${T}_pmc_$cfg.json \
     > $O/${T}_bench_$cfg.json 2> $O/${T}_bench_$cfg.err

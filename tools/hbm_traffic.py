@@ -33,6 +33,8 @@ def stage_of(kernel):
         return "prep"
     if "qkv_proj_kernel" in kernel:
         return "proj"
+    if "mx_gemm_kernel" in kernel:
+        return "proj_linear"
     return None
 
 
