@@ -489,9 +489,12 @@ def run_dropin(c, images, steps, warmup, device, world):
     import torch
     import mx_quantization_amd as M
     mx, funcs = M.install_dropin()
-    specs = {"w_elem_format": "int8", "a_elem_format": "int8", "scale_bits": 8, "shared_exp_method": "max",
-             "block_size": 32, "bfloat": 32, "round": "nearest", "round_mx_output": "nearest",
-             "round_output": "nearest", "round_weight": "nearest", "mx_flush_fp32_subnorms": False}
+    from mx_quantization_amd.mx.specs import apply_mx_specs
+    specs = apply_mx_specs({"w_elem_format": "int8", "a_elem_format": "int8", "scale_bits": 8,  # deit main.py:716-736
+                            "shared_exp_method": "max", "block_size": 32, "bfloat": 32, "fp": 0,
+                            "bfloat_subnorms": True, "round": "nearest", "round_mx_output": "nearest",
+                            "round_output": "nearest", "round_weight": "nearest",
+                            "mx_flush_fp32_subnorms": False, "custom_cuda": False, "quantize_backprop": False})
     t = lambda a: torch.from_numpy(a).to(device)
     q, k, v, _ = (None if a is None else t(a) for a in make_inputs(c, images))
 
