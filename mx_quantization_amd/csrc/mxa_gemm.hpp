@@ -77,7 +77,18 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int16_t* beb = a.be + bat * a.be_bat;
 
   // ---- per row / column of the tile: smallest finite block exponent, spread, NaN ----
-  // (rows / columns beyond the matrix: exponents 0, never NaN -- their results are dropped)
+  // (rows / columns beyond the matrix: exponents 0, never NaN -- their results are dropped).
+  // An all-zero block (shared exponent -126: code unit 2^-132 for int8, 2^-128 for int4)
+  // adds exactly 0 whatever its exponent: it is left out of the spread -- the pruned blocks of P in P.V would otherwise
+  // send every wave to the fp64 kernel.
+  const int8_t* abase = a.a + bat * a.a_bat;
+  const int8_t* bbase = a.b + bat * a.b_bat;
+  auto zero_blk = [&](bool isrow, int i, int kb, int e) {
+    if (e > -128 || e == kExpNaN) return false;
+    const int8_t* p = isrow ? abase + (int64_t)(m0g + i) * a.lda + 32 * kb : bbase + (int64_t)(n0g + i) * a.ldb + 32 * kb;
+    const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + 16);
+    return ((u.x | u.y | u.z | u.w) | (v.x | v.y | v.z | v.w)) == 0u;
+  };
   if (tid < kGemmRows + kGemmCols) {
     const bool isrow = tid < kGemmRows;
     const int i = isrow ? tid : tid - kGemmRows;
@@ -88,7 +99,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
         const int e = exp_from16(isrow ? aeb[(int64_t)(m0g + i) * nbk + kb] : beb[(int64_t)(n0g + i) * a.be_n + kb * a.be_k]);
         if (e == kExpNaN) {
           nan = 1;
-        } else {
+        } else if (!zero_blk(isrow, i, kb, e)) {
           lo = min(lo, e);
           hi = max(hi, e);
         }
@@ -102,12 +113,12 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   for (int i = tid; i < nbk * kGemmRows; i += 256) {
     const int kb = i / kGemmRows, r = i - kb * kGemmRows;
     int e = m0g + r < a.M ? exp_from16(aeb[(int64_t)(m0g + r) * nbk + kb]) : 0;
-    xe[i] = (int16_t)(e == kExpNaN ? 0 : e - rlo[r]);
+    xe[i] = (int16_t)(e == kExpNaN || zero_blk(true, r, kb, e) ? 0 : e - rlo[r]);
   }
   for (int i = tid; i < nbk * kGemmCols; i += 256) {
     const int kb = i / kGemmCols, c = i - kb * kGemmCols;
     int e = n0g + c < a.Nc ? exp_from16(beb[(int64_t)(n0g + c) * a.be_n + kb * a.be_k]) : 0;
-    ce[i] = (int16_t)(e == kExpNaN ? 0 : e - clo[c]);
+    ce[i] = (int16_t)(e == kExpNaN || zero_blk(false, c, kb, e) ? 0 : e - clo[c]);
   }
   __syncthreads();
 

@@ -279,71 +279,101 @@ __global__ __launch_bounds__(64 * kElsaWaves) void elsa_prep_kernel(ElsaPrepArgs
 
 // ---------------------------------------------------------------------------
 // approximator operand VALUES (what exponent_approximation's methods return)
-// one thread per (row, 32-block); exact fp32 op order of the reference.
+// one lane per element, 32 lanes per (row, 32-block): coalesced loads and stores, the
+// block's max |x| and max |code| by lane shuffles; exact fp32 op order of the reference.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lanes32_max(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int nb = (a.d + 31) / 32;
-  if (t >= a.rows * nb) return;
-  const int64_t row = t / nb;
-  const int blk = (int)(t % nb);
+  const int64_t bid = t >> 5;
+  const int j = (int)(t & 31);
+  const bool live = bid < a.rows * nb;  // every lane takes part in the shuffles
+  const int64_t row = live ? bid / nb : 0;
+  const int blk = live ? (int)(bid % nb) : 0;
+  const int c = blk * 32 + j;
+  const bool valid = live && c < a.d;
   const int dt = a.dt;
-  const int64_t xr = row * a.ld_x, yr = row * a.ld_out;
-  const int c0 = blk * 32, c1 = (c0 + 32 < a.d) ? c0 + 32 : a.d;
-  auto in = [&](int c) { return round_bfloat(load_dt(a.x, xr + c, dt), a.bfloat, kRoundNearest, 1, dt); };
-  uint32_t mb = 0;
-  for (int c = c0; c < c1; ++c) {
-    const uint32_t ub = __float_as_uint(in(c)) & 0x7FFFFFFFu;
-    mb = ub > mb ? ub : mb;
-  }
+  const float xin = valid ? round_bfloat(load_dt(a.x, row * a.ld_x + c, dt), a.bfloat, kRoundNearest, 1, dt) : 0.0f;
+  const uint32_t mb = lanes32_max(__float_as_uint(xin) & 0x7FFFFFFFu);
   int e_raw;
   const int es = scale_exponent_dt(mb, 127, dt, &e_raw);
   const bool nanblk = es == kExpNaN;
   const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
   const float qnan = __uint_as_float(0x7FC00000u);
-  int maxc = 0;
-  for (int c = c0; c < c1; ++c) {
-    float xv = in(c);
-    if (flush) xv = xv * 0.0f;
-    const int cd = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest, dt);
-    maxc = (cd < 0 ? -cd : cd) > maxc ? (cd < 0 ? -cd : cd) : maxc;
-  }
+  const float xv = flush ? xin * 0.0f : xin;
+  const int cd = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest, dt);
+  const int maxc = (int)lanes32_max((uint32_t)(cd < 0 ? -cd : cd));
   // exponent of the MX block (in the dtype: the MX max is a value of the dtype)
   const int eA = nanblk ? kExpNaN
                         : (maxc == 0 ? -126 : floor_log2_dt(__float_as_uint(round_dt((float)maxc * pow2f(es - 6), dt)), dt));
-  for (int c = c0; c < c1; ++c) {
-    float xv = in(c);
-    if (flush) xv = xv * 0.0f;
-    float out;
-    if (nanblk) {
-      out = a.op_kind == MXA_OP_TRUE_EX ? 1.0f : qnan;  // true_ex: NaN -> exponent 0 -> +1 (examples :98-110)
-    } else if (a.op_kind == MXA_OP_MXINT4) {
-      out = (round_code(xv, es, 4, kRoundNearest, dt) * 0.25f) * pow2f(es);
-    } else {
-      const int cd = (int)round_code(xv, es, 8, kRoundNearest, dt);
-      const float mxv = round_dt(((float)cd * pow2f(-6)) * pow2f(es), dt);  // MX int8 value
-      switch (a.op_kind) {
-        case MXA_OP_SIGN:  // (mx < 0 ? -1 : +1) * 2^eA
-          out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(eA);
-          break;
-        case MXA_OP_EXION: {  // sign(mx) * eA * (2^l1 + 2^l2) / 64
-          const int m = exion_m(cd << (es - eA));
-          const float sg = cd > 0 ? 1.0f : (cd < 0 ? -1.0f : 0.0f);
-          out = ((sg * (float)eA) * (float)(m < 0 ? -m : m)) / 64.0f;
-          break;
-        }
-        case MXA_OP_TRUE_EX: {  // (mx < 0 ? -1 : +1) * 2^(floor(log2|mx|)), zeros -> 2^0
-          const float am = fabsf(mxv);
-          const int te = am > 0.0f ? floor_log2_dt(__float_as_uint(am), dt) : 0;
-          out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(te);
-          break;
-        }
-        default:
-          out = mxv;
+  if (!valid) return;
+  float out;
+  if (nanblk) {
+    out = a.op_kind == MXA_OP_TRUE_EX ? 1.0f : qnan;  // true_ex: NaN -> exponent 0 -> +1 (examples :98-110)
+  } else if (a.op_kind == MXA_OP_MXINT4) {
+    out = (round_code(xv, es, 4, kRoundNearest, dt) * 0.25f) * pow2f(es);
+  } else {
+    const float mxv = round_dt(((float)cd * pow2f(-6)) * pow2f(es), dt);  // MX int8 value
+    switch (a.op_kind) {
+      case MXA_OP_SIGN:  // (mx < 0 ? -1 : +1) * 2^eA
+        out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(eA);
+        break;
+      case MXA_OP_EXION: {  // sign(mx) * eA * (2^l1 + 2^l2) / 64
+        const int m = exion_m(cd << (es - eA));
+        const float sg = cd > 0 ? 1.0f : (cd < 0 ? -1.0f : 0.0f);
+        out = ((sg * (float)eA) * (float)(m < 0 ? -m : m)) / 64.0f;
+        break;
       }
+      case MXA_OP_TRUE_EX: {  // (mx < 0 ? -1 : +1) * 2^(floor(log2|mx|)), zeros -> 2^0
+        const float am = fabsf(mxv);
+        const int te = am > 0.0f ? floor_log2_dt(__float_as_uint(am), dt) : 0;
+        out = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(te);
+        break;
+      }
+      default:
+        out = mxv;
     }
-    store_dt(a.out, yr + c, round_dt(out, dt), dt);
   }
+  store_dt(a.out, row * a.ld_out + c, round_dt(out, dt), dt);
+}
+
+// quantize_mx along a contiguous axis in 32-element blocks (the mx ops' axes=[-1] case):
+// one lane per element, the block max by lane shuffles -- quantize_mx_kernel's result
+__global__ __launch_bounds__(256) void quantize_mx_row32_kernel(QuantArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t bid = t >> 5;
+  const int j = (int)(t & 31);
+  const bool live = bid < a.outer * a.nb;
+  const int64_t o = live ? bid / a.nb : 0, blk = live ? bid % a.nb : 0;
+  const int64_t l = blk * 32 + j;
+  const bool valid = live && l < a.L;
+  const int64_t off = o * a.L + l;
+  float xv = valid ? round_bfloat(load_dt(a.x, off, a.dt), a.bfloat, kRoundNearest, 1, a.dt) : 0.0f;
+  const uint32_t mb = lanes32_max(__float_as_uint(xv) & 0x7FFFFFFFu);
+  int e_raw;
+  const int es = scale_exponent_dt(mb, a.scale_emax, a.dt, &e_raw);
+  if (!valid) return;
+  if (a.flush && !(e_raw != kExpNaN && e_raw > -127)) xv = xv * 0.0f;
+  const int shift = a.mbits - 2;
+  float yv, cv = 0.0f;
+  if (es == kExpNaN) {
+    yv = __uint_as_float(0x7FC00000u);
+  } else {
+    cv = round_code(xv, es, a.mbits, a.rnd, a.dt);
+    yv = (cv * pow2f(-shift)) * pow2f(es);
+  }
+  store_dt(a.y, off, yv, a.dt);  // (code * 2^(es-shift) rounded once to the dtype)
+  if (a.codes) a.codes[off] = (int8_t)cv;
+  if (a.exps && j == 0) a.exps[o * a.nb + blk] = exp_to16(es);
 }
 
 }  // namespace mxa
@@ -372,6 +402,10 @@ extern "C" int mxa_quantize_mx(const void* x, void* y, int8_t* codes, int16_t* e
   a.mbits = elem_mbits; a.scale_emax = (1 << (scale_bits - 1)) - 1; a.rnd = round_mode;
   a.flush = flush_subnormals; a.bfloat = bfloat; a.dt = dtype;
   const int64_t nblocks = outer * a.nb * inner;
+  if (inner == 1 && a.bs == 32) {  // contiguous 32-blocks: one lane per element
+    hipLaunchKernelGGL(quantize_mx_row32_kernel, dim3((unsigned)((nblocks * 32 + 255) / 256)), dim3(256), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+  }
   hipLaunchKernelGGL(quantize_mx_kernel, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
@@ -414,7 +448,8 @@ extern "C" int mxa_approx_values(const void* x, void* out, int64_t rows, int32_t
   ApproxArgs a{};
   a.x = x; a.out = out; a.rows = rows; a.d = d; a.ld_x = ld_x; a.ld_out = ld_out;
   a.op_kind = op_kind; a.flush = flush_subnormals; a.bfloat = bfloat; a.dt = dtype;
-  const int64_t n = rows * ((d + 31) / 32);
+  const int64_t n = rows * ((d + 31) / 32) * 32;  // one lane per element of the padded blocks
+  if (n / 256 >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(approx_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }

@@ -12,8 +12,8 @@ Differences from the reference, all deliberate:
     and partial_K/partial_Q (:284-293, :309-313) define the values (F2).
   * exponent_based_sign_leading_ones() ("true_ex") comes from the examples copy
     (:163-178), which the PixArt modules call.
-  * Methods do not `del` instance attributes (:92, :270); callers build a fresh
-    object per forward, so nothing observes the difference.
+  * Methods do not `del` instance attributes (:92, :270), and MX_Q / MX_K are built
+    on first use; callers build a fresh object per forward, so nothing observes either.
 Block size 32 (the workloads' mx_specs) is required.
 """
 from __future__ import annotations
@@ -36,11 +36,23 @@ class exponent_approximation:
         self.K = quantize_elemwise_op(K, mx_specs, round=mx_specs["round_output"])
         self.shared_exponent_method = mx_specs.get("shared_exp_method", "max")
         self._flush = bool(mx_specs["mx_flush_fp32_subnorms"])
-        # MXINT8 copies (funcs/exponent_based_prediction.py:18-31)
-        self.MX_Q = quantize_mx_op(self.Q, mx_specs, elem_format=mx_specs["a_elem_format"], axes=[-1],
-                                   round=mx_specs["round_mx_output"])
-        self.MX_K = quantize_mx_op(self.K, mx_specs, elem_format=mx_specs["a_elem_format"], axes=[-1],
-                                   round=mx_specs["round_mx_output"])
+
+    # MXINT8 copies (funcs/exponent_based_prediction.py:18-31): built on first use -- the
+    # approximators that do not read them (exp-sign, EXION, MXINT4, true_ex) skip two
+    # quantize launches per forward; the values are the same whenever they are read
+    @property
+    def MX_Q(self):
+        if "_MX_Q" not in self.__dict__:
+            self._MX_Q = quantize_mx_op(self.Q, self.mx_specs, elem_format=self.mx_specs["a_elem_format"], axes=[-1],
+                                        round=self.mx_specs["round_mx_output"])
+        return self._MX_Q
+
+    @property
+    def MX_K(self):
+        if "_MX_K" not in self.__dict__:
+            self._MX_K = quantize_mx_op(self.K, self.mx_specs, elem_format=self.mx_specs["a_elem_format"], axes=[-1],
+                                        round=self.mx_specs["round_mx_output"])
+        return self._MX_K
 
     # -- reference attributes, built on first use (:33-38) ----------------------
     def _blocks(self):
