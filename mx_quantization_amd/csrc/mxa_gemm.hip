@@ -67,6 +67,14 @@ int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int i
   g.b = reinterpret_cast<const int8_t*>(wb + W.rawc); g.ldb = W.Cpad;
   g.be = reinterpret_cast<const int16_t*>(wb + W.rawe); g.be_n = W.nbk; g.be_k = 1;
   g.M = (int)rows; g.Nc = out_f; g.nbk = W.nbk;
+  // the MFMA-ready codes when the buffer's column blocks are the output columns (one group,
+  // or groups of a multiple of 32 columns): its header's group width decides
+  LinearWeightHeader h{};
+  if (linear_weight_known_header(wq, &h) && (h.gw == out_f || h.gw % 32 == 0)) {
+    const LinearLayout P = linear_layout(out_f, in_f, h.gw);
+    g.bpk = reinterpret_cast<const int8_t*>(wb + P.pk);
+    g.b_nb32 = P.G * P.NB32;
+  }
   g.linear = 1; g.dt = kF32; g.bfloat = bfloat; g.autocast = autocast; g.bias = bias;
   g.c = out; g.ldc = out_row_stride;
   if (rows > ((int64_t)1 << 31) - 1) return MXA_ERR_UNSUPPORTED;

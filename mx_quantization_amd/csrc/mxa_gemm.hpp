@@ -159,9 +159,22 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int arow = min(m0g + wr0 + ln, a.M - 1);
   const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
   const int8_t* ap = a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
-  const int8_t* bp0 = a.b + bat * a.b_bat + (int64_t)bc0 * a.ldb + kh;
-  const int8_t* bp1 = a.b + bat * a.b_bat + (int64_t)bc1 * a.ldb + kh;
+  // B: row-major codes (lane: 16 B of its column at 32 kb + kh; K-block step 32 B), or the
+  // MFMA-ready pk layout (lane: 16 B at lane * 16 of its column block's 1-KB chunk; step 1 KB)
+  const int8_t *bp0, *bp1;
+  int bstep;
+  if (a.bpk) {
+    const int cb0 = min((n0g + wc0) / 32, a.b_nb32 - 1), cb1 = min((n0g + wc0 + 32) / 32, a.b_nb32 - 1);
+    bp0 = a.bpk + ((int64_t)cb0 * nbk * 64 + lane) * 16;
+    bp1 = a.bpk + ((int64_t)cb1 * nbk * 64 + lane) * 16;
+    bstep = 1024;
+  } else {
+    bp0 = a.b + bat * a.b_bat + (int64_t)bc0 * a.ldb + kh;
+    bp1 = a.b + bat * a.b_bat + (int64_t)bc1 * a.ldb + kh;
+    bstep = 32;
+  }
   auto ld = [](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + 32 * kb); };
+  auto ldb = [bstep](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + (int64_t)bstep * kb); };
   const v16i_g zero = {};
   const int last = nbk - 1;
   const int16_t* xrow = xe + wr0 + m0;
@@ -206,37 +219,30 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
         }
       }
     };
-    // operand slots: E = even blocks, O = odd blocks, each loaded two blocks ahead
-    v4i_g aE = ld(ap, 0), bE0 = ld(bp0, 0), bE1 = ld(bp1, 0);
-    v4i_g aO = ld(ap, min(1, last)), bO0 = ld(bp0, min(1, last)), bO1 = ld(bp1, min(1, last));
-    v16i_g cA0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE0, zero, 0, 0, 0);
-    v16i_g cA1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE1, zero, 0, 0, 0);
-    v16i_g cB0, cB1;
-    aE = ld(ap, min(2, last)); bE0 = ld(bp0, min(2, last)); bE1 = ld(bp1, min(2, last));
-    for (int kb = 0;; kb += 2) {
-      // cA holds block kb
+    // Pairs of K-blocks: the pair's four MFMAs are issued together, then the next pair's
+    // operands are loaded together (the A loads of blocks kb, kb + 1 touch the same 128-B
+    // line of each row, so it is fetched once), then the two epilogues run while those
+    // loads are in flight.  Operands of a pair: E (even block) and O (odd block) slots.
+    const int last2 = last;
+    v4i_g aE = ld(ap, 0), bE0 = ldb(bp0, 0), bE1 = ldb(bp1, 0);
+    v4i_g aO = ld(ap, min(1, last2)), bO0 = ldb(bp0, min(1, last2)), bO1 = ldb(bp1, min(1, last2));
+    for (int kb = 0; kb < nbk; kb += 2) {
       const bool h1 = kb + 1 < nbk;
+      const v16i_g cA0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE0, zero, 0, 0, 0);
+      const v16i_g cA1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE1, zero, 0, 0, 0);
+      v16i_g cB0 = zero, cB1 = zero;
       if (h1) {
         cB0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aO, bO0, zero, 0, 0, 0);
         cB1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aO, bO1, zero, 0, 0, 0);
-        const int kn = min(kb + 3, last);
-        aO = ld(ap, kn); bO0 = ld(bp0, kn); bO1 = ld(bp1, kn);
       }
+      const int ke = min(kb + 2, last2), ko = min(kb + 3, last2);
+      aE = ld(ap, ke); aO = ld(ap, ko);
+      bE0 = ldb(bp0, ke); bO0 = ldb(bp0, ko);
+      bE1 = ldb(bp1, ke); bO1 = ldb(bp1, ko);
       __builtin_amdgcn_sched_barrier(0);
       epi(cA0, cA1, kb);
+      if (h1) epi(cB0, cB1, kb + 1);
       __builtin_amdgcn_sched_barrier(0);
-      if (!h1) break;
-      const bool h2 = kb + 2 < nbk;
-      if (h2) {
-        cA0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE0, zero, 0, 0, 0);
-        cA1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aE, bE1, zero, 0, 0, 0);
-        const int kn = min(kb + 4, last);
-        aE = ld(ap, kn); bE0 = ld(bp0, kn); bE1 = ld(bp1, kn);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      epi(cB0, cB1, kb + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (!h2) break;
     }
     const int lc0 = clo[wc0 + ln], lc1 = clo[wc0 + 32 + ln];
 #pragma unroll
@@ -254,7 +260,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0.0;
       for (int kb = 0; kb < nbk; ++kb) {
-        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ld(bp, kb), zero, 0, 0, 0);
+        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ldb(bp, kb), zero, 0, 0, 0);
         const int dc = xcol[kb * kGemmCols + 32 * j] + lc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {

@@ -23,6 +23,8 @@ bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStr
 
 // does the prepared weight carry (out_f, in_f, flush, bfloat), whatever its group width?
 bool linear_weight_verify_any_group(const void* wq, int out_f, int in_f, int flush, int bfloat, hipStream_t stream);
+// the header of a prepared weight this process has seen (verified or prepared)
+bool linear_weight_known_header(const void* wq, LinearWeightHeader* h);
 // block-scaled MX GEMM (mxa_gemm.hip); mx.Linear on MX rows with a prepared weight
 // (slow: gemm_slow_bytes of device scratch for the list of waves the fp64 kernel takes)
 int64_t gemm_slow_bytes(int M, int Nc, int64_t batch);

@@ -188,6 +188,14 @@ bool linear_weight_verify(const void* wq, const LinearWeightHeader& want, hipStr
   return true;
 }
 
+bool linear_weight_known_header(const void* wq, LinearWeightHeader* h) {
+  std::lock_guard<std::mutex> g(g_wmu);
+  auto it = g_weights.find(wq);
+  if (it == g_weights.end()) return false;
+  *h = it->second;
+  return true;
+}
+
 bool linear_weight_verify_any_group(const void* wq, int out_f, int in_f, int flush, int bfloat, hipStream_t stream) {
   LinearWeightHeader h{};
   bool known = false;
