@@ -31,7 +31,7 @@ namespace mxa {
 constexpr int kGemmRows = 64, kGemmCols = 128;
 
 struct GemmLds {
-  size_t xe, ce, rlo, rn, clo, cn, total;
+  size_t xe, ce, rlo, rn, clo, cn, rhi, chi, part, total;
 };
 __host__ __device__ inline GemmLds gemm_lds(int nbk) {
   GemmLds L;
@@ -49,6 +49,12 @@ __host__ __device__ inline GemmLds gemm_lds(int nbk) {
   o += kGemmCols * 4;
   L.cn = o;
   o += kGemmCols * 4;
+  L.rhi = o;
+  o += kGemmRows * 4;
+  L.chi = o;
+  o += kGemmCols * 4;
+  L.part = o;  // prologue partials [3][256]
+  o += 3 * 256 * 4;
   L.total = o;
   return L;
 }
@@ -89,35 +95,86 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + 16);
     return ((u.x | u.y | u.z | u.w) | (v.x | v.y | v.z | v.w)) == 0u;
   };
-  if (tid < kGemmRows + kGemmCols) {
-    const bool isrow = tid < kGemmRows;
-    const int i = isrow ? tid : tid - kGemmRows;
-    const bool valid = isrow ? m0g + i < a.M : n0g + i < a.Nc;
+  // Per row 4 threads and per column 2 threads reduce strided K-block subsets (consecutive
+  // threads on consecutive exponents: coalesced, independent loads), partials through LDS.
+  int* chi = reinterpret_cast<int*>(smem + L.chi);
+  int* rhi_ = reinterpret_cast<int*>(smem + L.rhi);
+  int* part = reinterpret_cast<int*>(smem + L.part);  // [3][256]: lo, hi, nan per thread
+  const bool bk_major = a.be_k != 1;  // B exponents [kb][n] (cols_prep) vs [n][kb] (a weight)
+  auto a_exp = [&](int r, int kb) { return exp_from16(aeb[(int64_t)(m0g + r) * nbk + kb]); };
+  auto b_exp = [&](int c, int kb) { return exp_from16(beb[(int64_t)(n0g + c) * a.be_n + kb * a.be_k]); };
+  {
     int lo = 1 << 20, hi = -(1 << 20), nan = 0;
-    if (valid) {
-      for (int kb = 0; kb < nbk; ++kb) {
-        const int e = exp_from16(isrow ? aeb[(int64_t)(m0g + i) * nbk + kb] : beb[(int64_t)(n0g + i) * a.be_n + kb * a.be_k]);
+    auto take = [&](bool isrow, int i, int kb, int e) {
+      if (e == kExpNaN) {
+        nan = 1;
+      } else if (!zero_blk(isrow, i, kb, e)) {
+        lo = min(lo, e);
+        hi = max(hi, e);
+      }
+    };
+    // rows: thread (r = tid / 4, q = tid % 4) takes K-blocks q, q + 4, ...
+    {
+      const int r = tid >> 2, q = tid & 3;
+      if (m0g + r < a.M)
+        for (int kb = q; kb < nbk; kb += 4) take(true, r, kb, a_exp(r, kb));
+    }
+    part[tid] = lo;
+    part[256 + tid] = hi;
+    part[512 + tid] = nan;
+  }
+  __syncthreads();
+  if (tid < kGemmRows) {
+    int lo = 1 << 20, hi = -(1 << 20), nan = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lo = min(lo, part[4 * tid + q]);
+      hi = max(hi, part[256 + 4 * tid + q]);
+      nan |= part[512 + 4 * tid + q];
+    }
+    if (lo > hi) lo = hi = 0;
+    rlo[tid] = lo;
+    rhi_[tid] = hi;
+    rn[tid] = nan;
+  }
+  __syncthreads();
+  {
+    int lo = 1 << 20, hi = -(1 << 20), nan = 0;
+    // columns: [kb][n] exponents -- thread (c = tid % 128, half = tid / 128) takes K-blocks
+    // half, half + 2, ...; [n][kb] -- thread (c = tid / 2, half = tid % 2)
+    const int c = bk_major ? (tid & 127) : (tid >> 1), h = bk_major ? (tid >> 7) : (tid & 1);
+    if (n0g + c < a.Nc)
+      for (int kb = h; kb < nbk; kb += 2) {
+        const int e = b_exp(c, kb);
         if (e == kExpNaN) {
           nan = 1;
-        } else if (!zero_blk(isrow, i, kb, e)) {
+        } else if (!zero_blk(false, c, kb, e)) {
           lo = min(lo, e);
           hi = max(hi, e);
         }
       }
-    }
+    part[tid] = lo;
+    part[256 + tid] = hi;
+    part[512 + tid] = nan;
+  }
+  __syncthreads();
+  if (tid < kGemmCols) {
+    const int t0 = bk_major ? tid : 2 * tid, t1 = bk_major ? tid + 128 : 2 * tid + 1;
+    int lo = min(part[t0], part[t1]), hi = max(part[256 + t0], part[256 + t1]);
     if (lo > hi) lo = hi = 0;
-    (isrow ? rlo : clo)[i] = lo;
-    (isrow ? rn : cn)[i] = nan;
+    clo[tid] = lo;
+    chi[tid] = hi;
+    cn[tid] = part[512 + t0] | part[512 + t1];
   }
   __syncthreads();
   for (int i = tid; i < nbk * kGemmRows; i += 256) {
     const int kb = i / kGemmRows, r = i - kb * kGemmRows;
-    int e = m0g + r < a.M ? exp_from16(aeb[(int64_t)(m0g + r) * nbk + kb]) : 0;
+    const int e = m0g + r < a.M ? a_exp(r, kb) : 0;
     xe[i] = (int16_t)(e == kExpNaN || zero_blk(true, r, kb, e) ? 0 : e - rlo[r]);
   }
   for (int i = tid; i < nbk * kGemmCols; i += 256) {
     const int kb = i / kGemmCols, c = i - kb * kGemmCols;
-    int e = n0g + c < a.Nc ? exp_from16(beb[(int64_t)(n0g + c) * a.be_n + kb * a.be_k]) : 0;
+    const int e = n0g + c < a.Nc ? b_exp(c, kb) : 0;
     ce[i] = (int16_t)(e == kExpNaN || zero_blk(false, c, kb, e) ? 0 : e - clo[c]);
   }
   __syncthreads();
@@ -135,12 +192,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   };
   const int rr = wr0 + ln, cc = wc0 + lane;
   const bool rv = m0g + rr < a.M, cv = n0g + cc < a.Nc;
-  // spreads recomputed from the LDS offsets (row rr: lanes 0..31 and 32..63 alike)
-  int rsp = 0, csp = 0;
-  for (int kb = 0; kb < nbk; ++kb) {
-    rsp = max(rsp, (int)xe[kb * kGemmRows + rr]);
-    csp = max(csp, (int)ce[kb * kGemmCols + cc]);
-  }
+  // spreads (row rr: lanes 0..31 and 32..63 alike)
+  const int rsp = rhi_[rr] - rlo[rr], csp = chi[cc] - clo[cc];
   const int srow = wmax(rv ? rsp : 0), scol = wmax(cv ? csp : 0);
   const int lrow = wmin(rv ? rlo[rr] : (1 << 19)), lcol = wmin(cv ? clo[cc] : (1 << 19));
   const bool fast = srow + scol <= a.smax && lrow + lcol >= -126;
