@@ -137,7 +137,7 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
   }
   if (pj) {
     const int64_t C = (int64_t)p->H * p->D, nbk = (C + 31) / 32, tokens = (int64_t)p->B * p->N;
-    L.yc = take(tokens * nbk * 32);
+    L.yc = take((tokens + 31) / 32 * 32 * nbk * 32);  // MFMA-ready codes: whole 32-row blocks
     L.ys = take(tokens * nbk * 2);
     L.yf = take(proj_codes_direct(p) ? 0 : tokens * C * 4);
     L.yslow = take(gemm_slow_bytes((int)std::min<int64_t>(tokens, INT32_MAX), pj->out_features, 1));
@@ -411,12 +411,12 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
       ry.H = 1; ry.R = tokens; ry.rows = tokens; ry.D = C; ry.nb = nbk; ry.dpad = 32 * nbk;
       ry.vec4 = C % 4 == 0;
       ry.op_kind = MXA_OP_MXINT8; ry.flush = pp.flush_subnormals; ry.bfloat = pp.bfloat; ry.dt = MXA_DT_F32;
-      ry.codes = yc; ry.sT = ys;
+      ry.codes = yc; ry.sT = ys; ry.mfma_rows = 1;
       rc = launch_rows_prep(ry, stream);
       if (rc) return rc;
     }
     rc = launch_linear_codes(yc, ys, tokens, C, pj->wq, pj->out_features, pj->bias, pj->y, pj->y_row_stride,
-                             pp.bfloat, 0, reinterpret_cast<int*>(ws + L.yslow), stream);
+                             pp.bfloat, 0, reinterpret_cast<int*>(ws + L.yslow), stream, true);
     if (rc) return rc;
     if (ev) (void)hipEventRecord(ev[6], stream);
   }

@@ -367,6 +367,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
         ro.codes = a.xo_codes; ro.sT = a.xo_exps;
         ro.dpad = a.H * D; ro.nb = a.H * nbd; ro.D = a.H * D;
         ro.op_kind = MXA_OP_MXINT8; ro.flush = a.flush_p; ro.bfloat = a.bfloat; ro.dt = kF32;
+        ro.mfma_rows = 1;  // the MX GEMM's A layout
         const int64_t orow = (int64_t)b_ * a.N + (r < r_end ? r : r0);
         const int blk = h_ * nbd + dt / 32, c0 = h_ * D + dt + 16 * sub;
         if (rows_prep_plain(ro)) rows_prep_block_plain<16, kF32>(ro, orow, blk, sub, c0, xv, r < r_end);

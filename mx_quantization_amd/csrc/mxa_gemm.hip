@@ -59,11 +59,11 @@ int launch_gemm(const GemmArgs& ga, int64_t batch, int* slow, hipStream_t stream
 // prepared Linear weight (its row-major codes / exponents): out = mx.Linear epilogue
 int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int in_f, const void* wq, int out_f,
                         const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast, int* slow,
-                        hipStream_t stream) {
+                        hipStream_t stream, bool x_mfma) {
   const LinearLayout W = linear_layout(out_f, in_f, out_f);  // raw regions do not depend on gw
   const unsigned char* wb = static_cast<const unsigned char*>(wq);
   GemmArgs g{};
-  g.a = xc; g.ae = xs; g.lda = W.Cpad;
+  g.a = xc; g.ae = xs; g.lda = W.Cpad; g.a_mfma = x_mfma ? 1 : 0;
   g.b = reinterpret_cast<const int8_t*>(wb + W.rawc); g.ldb = W.Cpad;
   g.be = reinterpret_cast<const int16_t*>(wb + W.rawe); g.be_n = W.nbk; g.be_k = 1;
   g.M = (int)rows; g.Nc = out_f; g.nbk = W.nbk;
@@ -88,7 +88,8 @@ using namespace mxa;
 extern "C" int64_t mxa_linear_workspace_bytes(int64_t rows, int32_t in_features, int32_t out_features) {
   if (rows <= 0 || in_features <= 0 || out_features <= 0 || rows > INT32_MAX) return -1;
   const int64_t nbk = (in_features + 31) / 32;
-  return (rows * nbk * 32 + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256 +
+  const int64_t rows32 = (rows + 31) / 32 * 32;  // the MFMA-ready codes hold whole 32-row blocks
+  return (rows32 * nbk * 32 + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256 +
          gemm_slow_bytes((int)rows, out_features, 1);
 }
 
@@ -112,11 +113,13 @@ extern "C" int mxa_linear(const float* x, int64_t rows, int32_t in_features, int
   rx.H = 1; rx.R = rows; rx.rows = rows; rx.D = in_features; rx.nb = nbk; rx.dpad = Cpad;
   rx.vec4 = aligned16(x) && x_row_stride % 4 == 0;
   rx.op_kind = MXA_OP_MXINT8; rx.flush = flush_subnormals; rx.bfloat = bfloat; rx.dt = MXA_DT_F32;
+  const int64_t rows32 = (rows + 31) / 32 * 32;
   rx.codes = reinterpret_cast<int8_t*>(ws);
-  rx.sT = reinterpret_cast<int16_t*>(ws + (rows * Cpad + 255) / 256 * 256);
+  rx.mfma_rows = 1;
+  rx.sT = reinterpret_cast<int16_t*>(ws + (rows32 * Cpad + 255) / 256 * 256);
   int rc = launch_rows_prep(rx, stream);
   if (rc) return rc;
-  int* slow = reinterpret_cast<int*>(ws + (rows * Cpad + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256);
+  int* slow = reinterpret_cast<int*>(ws + (rows32 * Cpad + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256);
   return launch_linear_codes(rx.codes, rx.sT, rows, in_features, wq, out_features, bias, out, out_row_stride, bfloat,
-                             autocast_dtype, slow, stream);
+                             autocast_dtype, slow, stream, true);
 }

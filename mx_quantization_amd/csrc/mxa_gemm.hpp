@@ -91,8 +91,12 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int8_t* bbase = a.b + bat * a.b_bat;
   auto zero_blk = [&](bool isrow, int i, int kb, int e) {
     if (e > -128 || e == kExpNaN) return false;
-    const int8_t* p = isrow ? abase + (int64_t)(m0g + i) * a.lda + 32 * kb : bbase + (int64_t)(n0g + i) * a.ldb + 32 * kb;
-    const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + 16);
+    const int m = m0g + i;
+    const int8_t* p = !isrow   ? bbase + (int64_t)(n0g + i) * a.ldb + 32 * kb
+                      : a.a_mfma ? abase + (((int64_t)(m >> 5) * nbk + kb) * 64 + (m & 31)) * 16
+                                 : abase + (int64_t)m * a.lda + 32 * kb;
+    const int hoff = (isrow && a.a_mfma) ? 512 : 16;  // the block's second 16 elements
+    const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + hoff);
     return ((u.x | u.y | u.z | u.w) | (v.x | v.y | v.z | v.w)) == 0u;
   };
   // Per row 4 threads and per column 2 threads reduce strided K-block subsets (consecutive
@@ -211,7 +215,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
 
   const int arow = min(m0g + wr0 + ln, a.M - 1);
   const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
-  const int8_t* ap = a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
+  // A: row-major (lane: 16 B of its row at 32 kb + kh; K-block step 32 B), or the MFMA-ready
+  // row-block layout (lane: 16 B at lane * 16 of the wave's 1-KB chunk; step 1 KB)
+  const int8_t* ap = a.a_mfma ? a.a + (((int64_t)(m0g + wr0) >> 5) * nbk * 64 + lane) * 16
+                              : a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
+  const int astep = a.a_mfma ? 1024 : 32;
   // B: row-major codes (lane: 16 B of its column at 32 kb + kh; K-block step 32 B), or the
   // MFMA-ready pk layout (lane: 16 B at lane * 16 of its column block's 1-KB chunk; step 1 KB)
   const int8_t *bp0, *bp1;
@@ -226,7 +234,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     bp1 = a.b + bat * a.b_bat + (int64_t)bc1 * a.ldb + kh;
     bstep = 32;
   }
-  auto ld = [](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + 32 * kb); };
+  auto ld = [astep](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + (int64_t)astep * kb); };
   auto ldb = [bstep](const int8_t* p, int kb) { return *reinterpret_cast<const v4i_g*>(p + (int64_t)bstep * kb); };
   const v16i_g zero = {};
   const int last = nbk - 1;

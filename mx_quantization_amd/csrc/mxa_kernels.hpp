@@ -46,6 +46,9 @@ struct RowsPrepArgs {
   int16_t* sA;    // [rows][nb] approximator scale (nullable)
   uint32_t* signs;  // [rows][nb] bit i = (MX code i < 0) (nullable)
   int8_t* zind;     // [rows][dpad] 1 where the MX code is 0 (column < D), else 0 (true_ex; nullable)
+  int mfma_rows;    // codes layout: 0 row-major [rows][dpad]; 1 MFMA-ready for the MX GEMM's A operand,
+                    // [rows / 32][nb][lane][16 B] with lane = row % 32 + 32 * (16-element half)
+                    // (one coalesced 1-KB load per wave and K-block; rows padded to 32)
 };
 
 // ELSA sign hashes (and key norms) of rows already quantized by rows_prep:

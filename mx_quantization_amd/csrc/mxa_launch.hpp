@@ -31,6 +31,6 @@ int64_t gemm_slow_bytes(int M, int Nc, int64_t batch);
 int launch_gemm(const GemmArgs& ga, int64_t batch, int* slow, hipStream_t stream);
 int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int in_f, const void* wq, int out_f,
                         const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast, int* slow,
-                        hipStream_t stream);
+                        hipStream_t stream, bool x_mfma);
 
 }  // namespace mxa

@@ -111,7 +111,8 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       break;
   }
   if (valid) {
-    const int64_t base = row * a.dpad + c0;
+    const int64_t base = (EPL == 16 && a.mfma_rows) ? (((row >> 5) * a.nb + blk) * 64 + (row & 31) + 32 * sub) * 16
+                                                    : row * a.dpad + c0;
     uint32_t pc[EPL / 4], po[EPL / 4], pz[EPL / 4];
 #pragma unroll
     for (int w = 0; w < EPL / 4; ++w) {
@@ -196,7 +197,8 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
     for (int w = 0; w < EPL / 4; ++w)
       pc[w] = (uint32_t)(code[4 * w] & 0xFF) | (uint32_t)(code[4 * w + 1] & 0xFF) << 8 |
               (uint32_t)(code[4 * w + 2] & 0xFF) << 16 | (uint32_t)code[4 * w + 3] << 24;
-    const int64_t base = row * a.dpad + c0;
+    const int64_t base = (EPL == 16 && a.mfma_rows) ? (((row >> 5) * a.nb + blk) * 64 + (row & 31) + 32 * sub) * 16
+                                                    : row * a.dpad + c0;
     if constexpr (EPL == 16) {
       const uint4 v = make_uint4(pc[0], pc[1], pc[2], pc[3]);
       if (a.codes) *reinterpret_cast<uint4*>(a.codes + base) = v;
