@@ -217,7 +217,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
   // A: row-major (lane: 16 B of its row at 32 kb + kh; K-block step 32 B), or the MFMA-ready
   // row-block layout (lane: 16 B at lane * 16 of the wave's 1-KB chunk; step 1 KB)
-  const int8_t* ap = a.a_mfma ? a.a + (((int64_t)(m0g + wr0) >> 5) * nbk * 64 + lane) * 16
+  const int8_t* ap = a.a_mfma ? a.a + bat * a.a_bat + (((int64_t)(m0g + wr0) >> 5) * nbk * 64 + lane) * 16
                               : a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
   const int astep = a.a_mfma ? 1024 : 32;
   // B: row-major codes (lane: 16 B of its column at 32 kb + kh; K-block step 32 B), or the

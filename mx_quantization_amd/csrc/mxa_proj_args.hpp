@@ -94,7 +94,7 @@ struct GemmArgs {
   // blocks, [cb][kb][lane][16 B]): one coalesced 1-KB load per wave, chain and K-block
   const int8_t* bpk;
   int b_nb32;  // 32-column blocks in bpk
-  int a_mfma;  // A codes in rows_prep's MFMA-ready layout ([M / 32][nbk][lane][16 B]; a_bat, lda unused)
+  int a_mfma;  // A codes in rows_prep's MFMA-ready layout ([M / 32][nbk][lane][16 B] per batch; lda unused)
 };
 
 }  // namespace mxa
