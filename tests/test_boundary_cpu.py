@@ -159,3 +159,35 @@ def test_mismatch_analysis_vs_reference(tmp_path, monkeypatch):
     res = A.mismatch_analysis(str(ft), str(fp))
     assert str(res) == str(d["mm_name"])
     assert (tmp_path / str(res)).read_text() == str(d["mm_out"])
+
+
+def test_linear_and_proj_entry_points_validate_without_gpu():
+    """mxa_linear / mxa_attention_proj reject bad arguments before any HIP call, and the
+    workspace formulas: mxa_linear holds whole 32-row blocks of MFMA-ready codes; the
+    fused proj adds the proj input (codes + exponents, plus the fp32 copy when D % 32 != 0)
+    to the attention's workspace."""
+    import ctypes
+    from mx_quantization_amd import _native as N
+    lib = N.lib()
+    assert lib.mxa_linear(None, 10, 64, 64, None, 32, None, None, 32, 0, 0, 0, None, 0, None) == -1
+    assert lib.mxa_linear(1, 10, 64, 63, 1, 32, None, 1, 32, 0, 0, 0, None, 0, None) == -1  # row stride < in
+    assert lib.mxa_linear(1, 10, 64, 64, 1, 32, None, 1, 32, 0, 7, 0, None, 0, None) == -1  # bad bfloat
+    assert lib.mxa_linear_workspace_bytes(0, 64, 32) == -1
+    w = lib.mxa_linear_workspace_bytes(37, 100, 70)
+    assert w >= 64 * 128 + 37 * 4 * 2  # 2 row blocks x 4 K-blocks x 32 B, plus exponents
+    p = N.AttnParams()
+    p.B, p.H, p.N, p.T, p.D = 2, 12, 197, 197, 64
+    p.top_k, p.approx, p.k_top, p.pred_mode = 1, 1, 20, 0
+    pj = N.ProjParams()
+    pj.out_features = 768
+    base = lib.mxa_attention_workspace_bytes(ctypes.byref(p))
+    with_proj = lib.mxa_attention_proj_workspace_bytes(ctypes.byref(p), None, ctypes.byref(pj))
+    tokens32 = (2 * 197 + 31) // 32 * 32
+    assert with_proj >= base + tokens32 * 768 + 2 * 197 * 24 * 2
+    p.D, p.H = 72, 16  # a 32-block of C spans two heads: + the fp32 output copy
+    pj.out_features = 1152
+    base72 = lib.mxa_attention_workspace_bytes(ctypes.byref(p))
+    assert lib.mxa_attention_proj_workspace_bytes(ctypes.byref(p), None, ctypes.byref(pj)) >= base72 + 2 * 197 * 1152 * 4
+    assert lib.mxa_attention_proj(ctypes.byref(p), None, None, None) == -1  # no proj params
+    pj.wq = None
+    assert lib.mxa_attention_proj(ctypes.byref(p), None, ctypes.byref(pj), None) == -1  # no weight
