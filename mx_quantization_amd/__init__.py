@@ -33,7 +33,9 @@ from .ops import (  # noqa: F401
     unpack_mask,
 )
 
-__all__ = ["mx_topk_attention", "mx_qkv_attention", "mx_topk_attention_proj", "mx_linear", "LinearWeightMX", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
+from .exact_topk import TORCH as exact_topk_torch, bind_exact_topk, unbind_exact_topk  # noqa: F401,E402
+
+__all__ = ["bind_exact_topk", "unbind_exact_topk", "exact_topk_torch", "mx_topk_attention", "mx_qkv_attention", "mx_topk_attention_proj", "mx_linear", "LinearWeightMX", "mx_approx_scores", "topk", "unpack_mask", "quantize_mx", "mx_matmul", "install_dropin", "NativeError"]
 
 
 def install_dropin():

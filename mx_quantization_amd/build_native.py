@@ -20,7 +20,7 @@ UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", ""
          ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
-           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
+           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
            "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

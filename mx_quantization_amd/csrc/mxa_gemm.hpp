@@ -217,7 +217,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
   // A: row-major (lane: 16 B of its row at 32 kb + kh; K-block step 32 B), or the MFMA-ready
   // row-block layout (lane: 16 B at lane * 16 of the wave's 1-KB chunk; step 1 KB)
-  const int8_t* ap = a.a_mfma ? a.a + bat * a.a_bat + (((int64_t)(m0g + wr0) >> 5) * nbk * 64 + lane) * 16
+  // (the row block clamped to the last one that exists: when M % 64 is 1..32 the second
+  // wave of the last row tile has no rows, and the layout holds whole 32-row blocks only)
+  const int8_t* ap = a.a_mfma ? a.a + bat * a.a_bat + ((int64_t)min((m0g + wr0) >> 5, (a.M - 1) >> 5) * nbk * 64 + lane) * 16
                               : a.a + bat * a.a_bat + (int64_t)arow * a.lda + kh;
   const int astep = a.a_mfma ? 1024 : 32;
   // B: row-major codes (lane: 16 B of its column at 32 kb + kh; K-block step 32 B), or the
@@ -252,8 +254,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     if constexpr (PLAIN) {
       static_cast<float*>(a.c)[off] = a.bias ? o + a.bias[n] : o;
     } else if (a.linear) {
-      o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
-      o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
+      // autocast: F.linear returns the dtype, then the output rounding (linear.py:88-92),
+      // then + fp32 bias promotes back (the same order as the mx.matmul branch below)
+      o = round_bfloat(round_dt(o, a.autocast), a.bfloat, kRoundNearest, 1, a.autocast);
       if (a.bias) o = round_bfloat(o + round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1), a.bfloat, kRoundNearest, 1);
       static_cast<float*>(a.c)[off] = o;
     } else {

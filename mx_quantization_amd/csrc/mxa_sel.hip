@@ -27,8 +27,27 @@ static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, boo
   hipLaunchKernelGGL((select_kernel<NP, MODE, W>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
+// ---- selection kernel, one wave per query row (mxa_select.hpp select_wave_kernel) ----
+template <int NP, int MODE>
+static int launch_select_wave(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
+  Rows2Args ra = ra0;
+  const size_t lds = selw_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd);
+  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  if (plan) return MXA_OK;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_wave_kernel<NP, MODE>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
+  int rows = kSelRows;
+  while (rows > kSelWaveW && (int64_t)BH * ((ra.N + rows - 1) / rows) < 4096) rows -= kSelWaveW;
+  ra.rows_per_wg = rows;
+  const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
+  hipLaunchKernelGGL((select_wave_kernel<NP, MODE>), dim3((unsigned)BH, gy), dim3(64 * kSelWaveW), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (MXA_SEL_WAVE) return launch_select_wave<NP, MODE>(ra, BH, stream, plan);
   if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
   return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
 }
@@ -74,6 +93,15 @@ using namespace mxa;
 
 // ---- standalone top-k: one DPP row per row (mxa_topk_grp.hpp) -----------------------
 template <int NP>
+static int launch_topk_wave(const GrpTopkArgs& ga, hipStream_t stream) {
+  const size_t lds = (size_t)4 * wrow_bytes(ga.n);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_wave_kernel<NP>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL(topk_wave_kernel<NP>, dim3((unsigned)((ga.rows + 3) / 4)), dim3(256), lds, stream, ga);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NP>
 static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t stream) {
   const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_grp_kernel<NP>),
@@ -95,6 +123,11 @@ extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, i
     return MXA_OK;
   }
   const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
+  if (MXA_SEL_WAVE) {
+    if (n <= 128) return launch_topk_wave<128>(ga, stream);
+    if (n <= 256) return launch_topk_wave<256>(ga, stream);
+    return launch_topk_wave<512>(ga, stream);
+  }
   const unsigned grid = (unsigned)((rows + 15) / 16);
   if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
   if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);

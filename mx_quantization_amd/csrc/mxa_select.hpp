@@ -23,6 +23,7 @@
 #include <type_traits>
 #include "mxa_rows2.hpp"
 #include "mxa_topk_grp.hpp"
+#include "mxa_topk_wave.hpp"
 
 namespace mxa {
 
@@ -31,6 +32,12 @@ namespace mxa {
 #endif
 #ifndef MXA_SEL_OCC
 #define MXA_SEL_OCC 4
+#endif
+#ifndef MXA_SELW_OCC
+#define MXA_SELW_OCC 8
+#endif
+#ifndef MXA_SEL_WAVE  // 1: one wave per query row (select_wave_kernel); 0: four rows per wave (A/B builds)
+#define MXA_SEL_WAVE 1
 #endif
 #ifndef MXA_SEL_SHORT_T
 #define MXA_SEL_SHORT_T 224
@@ -426,6 +433,219 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
+// ---- the selection kernel, ONE WAVE PER QUERY ROW (mxa_topk_wave.hpp) ------------
+// Per workgroup (one head, a chunk of its query rows, kSelWaveW waves): the score
+// tables staged in LDS as above; then each wave takes rows wave, wave + W, ...: lane
+// computes the scores of keys lane, lane + 64, ... into the row's mirror, wave_topk
+// reproduces torch's CPU index order with the row's bookkeeping in scalar registers,
+// and the k kept indices (int64 + int32) and the prune-mask words go out.  The query
+// row's operands are wave-uniform (scalar loads).
+constexpr int kSelWaveW = 4;
+__host__ __device__ inline size_t selw_lds(int mode, int T, int D, int kst, int nbd) {
+  return sel_lds(mode, T, D, kst, nbd).rows + (size_t)kSelWaveW * wrow_bytes(T);
+}
+
+template <int NP, int MODE>
+__global__ __launch_bounds__(64 * kSelWaveW) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : 4, 8))) void select_wave_kernel(Rows2Args a0) {
+  const Rows2Args& a = a0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
+  constexpr int EW = NP / 64;
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t lane0 = threadIdx.x & 63;
+  const int bh = blockIdx.x;
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
+  const int b_ = bh / a.H, h_ = bh % a.H;
+  const SelLds L = sel_lds(MODE, T, D, kst, nbd);
+  int8_t* tcd = reinterpret_cast<int8_t*>(smem + L.cd);
+  int16_t* tex = reinterpret_cast<int16_t*>(smem + L.ex);
+  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
+  int8_t* tz = reinterpret_cast<int8_t*>(smem + L.z);
+  float* tcs = reinterpret_cast<float*>(smem + L.cs);
+
+  // ---- stage the head's score tables ----------------------------------------
+  const int64_t kb = (int64_t)bh * T;
+  if constexpr (MODE == kModeTrue || kOp || MODE == kModeTrueEx) {
+    const int8_t* src = MODE == kModeTrue ? a.kc : a.kop;
+    const int cpr = a.dpad / 16;
+    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
+      const int j = i / cpr, c = i - j * cpr;
+      *reinterpret_cast<uint4*>(tcd + (size_t)j * kst + 16 * c) =
+          *reinterpret_cast<const uint4*>(src + (kb + j) * a.dpad + 16 * c);
+      if (MODE == kModeTrueEx)
+        *reinterpret_cast<uint4*>(tz + (size_t)j * kst + 16 * c) =
+            *reinterpret_cast<const uint4*>(a.kz + (kb + j) * a.dpad + 16 * c);
+    }
+  }
+  {
+    const int16_t* esrc = MODE == kModeTrue ? a.ksT : a.ksA;
+    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
+      if (MODE != kModeElsa) tex[i] = esrc[kb * nbd + i];
+      if (MODE == kModeExSign || MODE == kModeElsa) tsg[i] = a.ksg[kb * nbd + i];
+    }
+    if (MODE == kModeElsa)
+      for (int h = threadIdx.x; h <= D; h += blockDim.x) tcs[h] = a.elsa_cos ? a.elsa_cos[h] : elsa_cos_entry(D, h);
+  }
+  __syncthreads();
+
+  const WRow g = carve_wrow(smem + L.rows + (size_t)wave * wrow_bytes(T), T);
+  const int ntw = (T + 31) / 32;  // prune-mask words per row
+  const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
+  for (int r = (int)blockIdx.y * a.rows_per_wg + wave; r < r_end; r += kSelWaveW) {
+    // the argument block re-read per row (scalar loads, cache hits) rather than held in
+    // SGPRs across the top-k: SGPRs bound the resident waves
+    typedef __attribute__((address_space(4))) const Rows2Args KArgs;
+    KArgs* ap = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));
+    KArgs& a = *ap;
+    uint32_t lane = lane0;  // (re-derived per row as well: its hoisted address arithmetic spilled)
+    asm volatile("" : "+v"(lane));
+    // (every size re-read too: hoisted, the top-k's conditions on k and T were spilled)
+    const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
+    const int64_t kb = (int64_t)bh * T;
+    const int64_t grow = (int64_t)bh * a.N + r;
+    const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : -1;
+
+    // ---- the row's scores into its mirror ------------------------------------
+    auto emit = [&](int j, float v) {
+      v = round_dt(v, a.s_dt);
+      if (brow >= 0) v = round_dt(v + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
+      if (MODE == kModeTrue) {
+        if (a.true_out) a.true_out[grow * T + j] = v;
+      } else if (a.pred_out) {
+        a.pred_out[grow * T + j] = v;
+      }
+      g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+    };
+    if constexpr (MODE == kModeExSign) {
+      // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
+      uint32_t sq[kMaxNB];
+      int eq[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) {
+        sq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
+        eq[b] = b < nbd ? s_exp16(a.qsA, grow * nbd + b) : 0;
+      }
+      auto keys = [&](auto nbd_c) {
+        constexpr int NBD = decltype(nbd_c)::value;
+        if (brow >= 0 || a.s_dt != kF32) {
+          for (int j = (int)lane; j < T; j += 64) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
+          return;
+        }
+        int eqr[NBD], nbk[NBD];
+#pragma unroll
+        for (int b = 0; b < NBD; ++b) {
+          eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
+          nbk[b] = min(32, D - 32 * b);
+        }
+        float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
+        for (int j = (int)lane; j < T; j += 64) {
+          const int16_t* kex = tex + j * NBD;
+          const uint32_t* ksg = tsg + j * NBD;
+          int e[NBD], m[NBD];
+#pragma unroll
+          for (int b = 0; b < NBD; ++b) {
+            e[b] = eqr[b] + (int)kex[b];
+            m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
+          }
+          int emin = e[0], emax = e[0];
+#pragma unroll
+          for (int b = 1; b < NBD; ++b) {
+            emin = min(emin, e[b]);
+            emax = max(emax, e[b]);
+          }
+          float v;
+          uint32_t key;
+          if (emax - emin <= 23 && emin >= -100) {
+            int sum = 0;
+#pragma unroll
+            for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
+            v = ldexpf((float)sum, emin);
+            const uint32_t u = __float_as_uint(v);
+            key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
+          } else {
+            v = expred_score<NBD>(sq, eq, kex, ksg, D);
+            key = order_key(v);
+          }
+          if (prow) prow[j] = v;
+          g.A[j] = pack_ki(key, (uint32_t)j);
+        }
+      };
+      switch (nbd) {
+        case 1: keys(std::integral_constant<int, 1>{}); break;
+        case 2: keys(std::integral_constant<int, 2>{}); break;
+        case 3: keys(std::integral_constant<int, 3>{}); break;
+        default: keys(std::integral_constant<int, 4>{}); break;
+      }
+    } else if constexpr (MODE == kModeElsa) {
+      uint32_t hq[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) hq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
+      const float nrm = a.knorm[kb + r];
+      for (int j = (int)lane; j < T; j += 64) {
+        int h = 0;
+#pragma unroll
+        for (int b = 0; b < kMaxNB; ++b)
+          if (b < nbd) h += (int)__popc(hq[b] ^ tsg[j * nbd + b]);
+        emit(j, nrm * tcs[h]);
+      }
+    } else {
+      const int8_t* qsrc = (MODE == kModeTrue ? a.qc : a.qop) + grow * a.dpad;
+      const int16_t* qesrc = MODE == kModeTrue ? a.qsT : a.qsA;
+      uint4 qv[2 * kMaxNB];
+      uint4 qz[MODE == kModeTrueEx ? 2 * kMaxNB : 1];
+      int qe[kMaxNB];
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b) {
+        const cu32 qw = (cu32)(qsrc + 32 * b);
+        qv[2 * b] = b < nbd ? make_uint4(qw[0], qw[1], qw[2], qw[3]) : make_uint4(0, 0, 0, 0);
+        qv[2 * b + 1] = b < nbd ? make_uint4(qw[4], qw[5], qw[6], qw[7]) : make_uint4(0, 0, 0, 0);
+        if constexpr (MODE == kModeTrueEx) {
+          const cu32 zw = (cu32)(a.qz + grow * a.dpad + 32 * b);
+          qz[2 * b] = b < nbd ? make_uint4(zw[0], zw[1], zw[2], zw[3]) : make_uint4(0, 0, 0, 0);
+          qz[2 * b + 1] = b < nbd ? make_uint4(zw[4], zw[5], zw[6], zw[7]) : make_uint4(0, 0, 0, 0);
+        }
+        qe[b] = b < nbd ? s_exp16(qesrc, grow * nbd + b) : 0;
+      }
+      for (int j = (int)lane; j < T; j += 64) {
+        bool nan = false;
+        double acc;
+        if constexpr (MODE == kModeTrueEx)
+          acc = g_dot_trueex(qv, qz, qe, nbd, tcd + (size_t)j * kst, tz + (size_t)j * kst, tex + j * nbd, nan);
+        else
+          acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
+        float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+        if (MODE == kModeTrue) v = round_bfloat(round_dt(v, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt) * a.scale;
+        emit(j, v);
+      }
+    }
+    if (k <= 0) continue;  // scores only
+    wave_lds_sync();
+
+    // ---- torch CPU top-k order ------------------------------------------------
+    wave_topk<EW>(g, T, k);
+
+    // ---- kept indices, prune mask ----------------------------------------------
+    for (int p = (int)lane; p < k; p += 64) {
+      const uint32_t ix = (uint32_t)g.A[p];
+      if (a.idx_out) a.idx_out[grow * k + p] = (int64_t)ix;
+      a.idx32[grow * k + p] = (int32_t)ix;
+    }
+    if (a.mask_out) {  // prune mask: zeros.scatter_(-1, idx, 1) as bits
+      wl32* mw = (wl32*)g.SL;  // free after the top-k
+      if ((int)lane < ntw) mw[lane] = 0u;
+      wave_lds_sync();
+      for (int p = (int)lane; p < k; p += 64) {
+        const uint32_t ix = (uint32_t)g.A[p];
+        atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
+      }
+      wave_lds_sync();
+      if ((int)lane < ntw) a.mask_out[grow * ntw + lane] = mw[lane];
+    }
+    wave_lds_sync();
+  }
+}
+
 // ---- standalone top-k over rows of a float matrix (mxa_topk) ------------------
 struct GrpTopkArgs {
   const void* vals;  // dtype dt
@@ -470,6 +690,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
     wave_lds_sync();
     if (valid)
       for (int w = gl; w < ntw; w += 16) a.out_mask[row * ntw + w] = mw[w];
+  }
+}
+
+// one wave per row (mxa_topk_wave.hpp): waves of a 256-thread workgroup take rows
+// 4 blockIdx.x + wave
+template <int NP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : 4, 8))) void topk_wave_kernel(GrpTopkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = (int)(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= a.rows) return;
+  const WRow g = carve_wrow(smem + (size_t)wave * wrow_bytes(a.n), a.n);
+  const int64_t src = row * a.ld;
+  for (int j = (int)lane; j < a.n; j += 64) g.A[j] = pack_ki(order_key(load_dt(a.vals, src + j, a.dt)), (uint32_t)j);
+  wave_lds_sync();
+  wave_topk<NP / 64>(g, a.n, a.k);
+  for (int p = (int)lane; p < a.k; p += 64) {
+    const uint32_t ix = (uint32_t)g.A[p];
+    a.out_idx[row * a.k + p] = (int64_t)ix;
+    if (a.out_vals) store_dt(a.out_vals, row * a.k + p, load_dt(a.vals, src + ix, a.dt), a.dt);
+  }
+  if (a.out_mask) {
+    const int ntw = (a.n + 31) / 32;
+    wl32* mw = (wl32*)g.SL;
+    if ((int)lane < ntw) mw[lane] = 0u;
+    wave_lds_sync();
+    for (int p = (int)lane; p < a.k; p += 64) {
+      const uint32_t ix = (uint32_t)g.A[p];
+      atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
+    }
+    wave_lds_sync();
+    if ((int)lane < ntw) a.out_mask[row * ntw + lane] = mw[lane];
   }
 }
 

@@ -17,18 +17,37 @@ from .matmul import _check_specs, _mbits
 from .specs import apply_mx_specs, mx_assert_test
 
 
-_PREPARED = {}  # (weight storage, version, flush, bfloat) -> LinearWeightMX
+# id(weight) -> (weakref to the weight, stamp, LinearWeightMX).  The entry belongs to
+# the weight OBJECT (the weakref must still resolve to it), so a new tensor that the
+# caching allocator puts at a freed weight's address never sees the old codes, and an
+# entry dies with its weight (weakref callback).  The stamp adds what can change in
+# place: storage address, shape, strides, device, the autograd version counter and the
+# specs.  In-place writes that bypass the version counter (`param.data.copy_(...)`) are
+# invisible to it: call invalidate_prepared() after them.
+_PREPARED = {}
+
+
+def invalidate_prepared(weight=None):
+    """Drop the prepared MX codes of `weight` (all weights when None)."""
+    if weight is None:
+        _PREPARED.clear()
+    else:
+        _PREPARED.pop(id(weight), None)
 
 
 def _prepared_weight(weight, s):
     """The weight's MX codes, prepared once per weight version (inference: constant)."""
-    key = (weight.data_ptr(), tuple(weight.shape), weight._version, bool(s["mx_flush_fp32_subnorms"]), int(s["bfloat"]))
-    wq = _PREPARED.get(key)
-    if wq is None:
-        if len(_PREPARED) > 256:
-            _PREPARED.clear()
-        wq = ops.LinearWeightMX(weight.detach().contiguous(), weight.shape[0], s["mx_flush_fp32_subnorms"], s["bfloat"])
-        _PREPARED[key] = wq
+    import weakref
+    stamp = (weight.data_ptr(), tuple(weight.shape), tuple(weight.stride()), str(weight.device), weight._version,
+             bool(s["mx_flush_fp32_subnorms"]), int(s["bfloat"]))
+    ent = _PREPARED.get(id(weight))
+    if ent is not None and ent[0]() is weight and ent[1] == stamp:
+        return ent[2]
+    wq = ops.LinearWeightMX(weight.detach().contiguous(), weight.shape[0], s["mx_flush_fp32_subnorms"], s["bfloat"])
+    wid = id(weight)
+    ref = weakref.ref(weight, lambda _r, wid=wid: _PREPARED.pop(wid, None) if _PREPARED.get(wid, (None,))[0] is _r
+                      else None)
+    _PREPARED[wid] = (ref, stamp, wq)
     return wq
 
 

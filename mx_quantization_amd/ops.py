@@ -411,7 +411,10 @@ def mx_linear(x: torch.Tensor, weight, bias: Optional[torch.Tensor] = None, flus
     check(lib().mxa_linear(x2.data_ptr(), rows, wq.in_features, x2.stride(0), wq.buf.data_ptr(), wq.out_features,
                            bptr, out.data_ptr(), out.stride(0), int(bool(flush_subnormals)), int(bfloat), ac,
                            ws.data_ptr(), ws.numel(), stream_ptr(dev)), "mxa_linear")
-    return out.reshape(x.shape[:-1] + (wq.out_features,))
+    out = out.reshape(x.shape[:-1] + (wq.out_features,))
+    if ac and bias is None:  # F.linear's autocast dtype (the values are already rounded to it)
+        out = out.to(autocast)
+    return out
 
 
 def _proj_params(proj_weight, proj_bias, C: int, rows: int, flush_subnormals: bool, bfloat: int, dev):

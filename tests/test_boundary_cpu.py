@@ -191,3 +191,26 @@ def test_linear_and_proj_entry_points_validate_without_gpu():
     assert lib.mxa_attention_proj(ctypes.byref(p), None, None, None) == -1  # no proj params
     pj.wq = None
     assert lib.mxa_attention_proj(ctypes.byref(p), None, ctypes.byref(pj), None) == -1  # no weight
+
+
+def test_exact_topk_bind_cpu():
+    """bind_exact_topk rebinds only a module-level `torch` that is torch itself; the
+    namespace forwards everything else; CPU tensors get torch's own topk (the reference's
+    CPU path)."""
+    import types
+
+    import torch
+
+    import mx_quantization_amd as M
+    mod = types.ModuleType("glue")
+    mod.torch = torch
+    other = {"torch": "not torch"}
+    assert M.bind_exact_topk(mod, other) == 1
+    assert mod.torch is M.exact_topk_torch and other["torch"] == "not torch"
+    assert mod.torch.softmax is torch.softmax and mod.torch.return_types is torch.return_types
+    x = torch.randn(4, 50)
+    r = mod.torch.topk(x, 7, dim=-1, largest=True, sorted=True)
+    w = torch.topk(x, 7)
+    assert torch.equal(r.indices, w.indices) and torch.equal(r.values, w.values)
+    M.unbind_exact_topk(mod)
+    assert mod.torch is torch

@@ -486,8 +486,46 @@ def test_linear_dropin(M):
     lin = mx.Linear(96, 80, bias=True, mx_specs=specs).cuda()
     x = torch.randn(2, 7, 96, device="cuda")
     y = lin(x)
-    want = O.mx_matmul(host(x), host(lin.weight).T) + host(lin.bias)
-    assert np.max(np.abs(host(y) - want)) <= 1e-5 * max(1.0, np.abs(want).max())
+    same(host(y), O.mx_linear(host(x), host(lin.weight), host(lin.bias)), "mx.Linear drop-in")
+
+
+@pytest.mark.parametrize("case,mode,approx,k_top", [("ex_pred_k20", "ex_pred", True, 20),
+                                                    ("partial_Q_k20", "partial_Q", True, 20),
+                                                    ("MXINT4_k20", "MXINT4", True, 20),
+                                                    ("trueK_k30", None, False, 30)])
+def test_unchanged_glue_exact_topk(M, case, mode, approx, k_top):
+    """The DeiT glue (main.py:100-152, tests/glue_deit.py) run unchanged on the drop-in
+    modules, its own `torch.topk` call served by bind_exact_topk: idx bit-exact against the
+    reference's (attn_deit_tiny.npz), the output within tolerance."""
+    M.install_dropin()
+    import glue_deit
+    from mx.specs import apply_mx_specs
+    d = load("attn_deit_tiny.npz")
+    specs = apply_mx_specs({"a_elem_format": "int8", "w_elem_format": "int8", "block_size": 32, "scale_bits": 8,
+                            "bfloat": 32, "shared_exp_method": "max", "round": "nearest"})
+    assert M.bind_exact_topk(glue_deit) == 1
+    try:
+        out, idx = glue_deit.attention_core(dev(d["q"]), dev(d["k"]), dev(d["v"]), float(d["scale"]), k_top, specs,
+                                            pred_mode=mode or "ex_pred", approx=approx)
+    finally:
+        M.unbind_exact_topk(glue_deit)
+    torch.cuda.synchronize()
+    same(host(idx), d[f"{case}/idx"], f"{case} idx through the module's torch.topk")
+    assert O.normwise_rel_err(host(out), d[f"{case}/out"]) <= OUT_TOL
+    assert glue_deit.torch is torch
+
+
+def test_exact_topk_namespace_forwards(M):
+    """The rebound name is torch for everything but topk; unsupported topk forms are torch's."""
+    T = M.exact_topk_torch
+    assert T.zeros is torch.zeros and T.cuda is torch.cuda and T.float32 is torch.float32
+    x = torch.randn(3, 40, device="cuda")
+    r = T.topk(x, 5, dim=-1, largest=False)
+    same(host(r.indices), host(torch.topk(x, 5, dim=-1, largest=False).indices), "largest=False passthrough")
+    v, i = T.topk(x, 5)
+    _, want = O.topk(host(x), 5)
+    same(host(i), want, "exact order")
+    same(host(v), np.take_along_axis(host(x), want, -1), "values")
 
 
 # ------------------------------------------------------------------ fused qkv projection

@@ -175,3 +175,45 @@ def test_bench_limiter_from_profiles(tmp_path):
     pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("2>", "4>"): {"SQ_INSTS_VALU": 1.0}}))
     _, lim = bench.profile_of({"pmc": str(pj)}, "select", 0.5, 320.0)
     assert "kernel" not in lim and lim["bound"] == "hbm"
+
+
+def _dit_worker(rank, world, port, argv, out):
+    """bench.main on the DiT-XL/2 config (2 heads per image to keep the oracle cheap); the
+    stand-in records which images this rank generated and checks them against the
+    images a 1-rank run generates for the same ids."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), MXA_BENCH_BACKEND="gloo")
+    import bench
+    bench.CONFIGS["dit_xl2"] = dict(bench.CONFIGS["dit_xl2"], H=2)
+
+    def run(c, images, steps, warmup, device, world_, prof):
+        out[f"images{rank}"] = list(images)
+        q, k, v, _ = bench.make_inputs(c, images)
+        q1, k1, v1, _ = bench.make_inputs(c, list(range(c["B"])))  # the 1-rank run's batch
+        out[f"same{rank}"] = bool(np.array_equal(q, q1[images]) and np.array_equal(k, k1[images])
+                                  and np.array_equal(v, v1[images]))
+        return _stub_run(c, images, steps, warmup, device, world_, prof)
+
+    res = bench.main(argv, run=run)
+    if rank == 0:
+        out["res"] = json.dumps(res)
+    dist.destroy_process_group()
+
+
+def test_bench_dit_strong_scaling_two_ranks_shard_boundaries():
+    """configs[3] (DiT-XL/2 sharded over GPUs, strong scaling): B = 64 over 2 ranks is
+    images 0-31 and 32-63, each rank's inputs equal the 1-rank run's images, the job
+    reports the whole batch, and rank 0 checks a sample of both shards."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    argv = ["--config", "dit_xl2", "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-secondary",
+            "--scaling", "strong", "--parity-images", "1", "--no-cpu-baseline"]
+    mp.spawn(_dit_worker, args=(2, port, argv, out), nprocs=2, join=True)
+    assert out["images0"] == list(range(32)) and out["images1"] == list(range(32, 64))
+    assert out["same0"] and out["same1"]
+    res = json.loads(out["res"])
+    assert res["config"]["global_batch"] == 64 and res["config"]["batch_per_gpu"] == 32
+    assert res["scaling"] == "strong" and res["n_gpus"] == 2
+    assert res["value"] == pytest.approx(64 * 256 * 2 / (res["ms_per_step"] * 2 / 1e3))
+    assert res["parity"]["ranks_checked"] == 2 and res["parity"]["idx_bitmatch"] == 1.0

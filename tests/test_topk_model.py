@@ -60,3 +60,26 @@ def test_model_depth_limit_fallbacks(n, k):
     assert np.array_equal(got, want[0])
     if k >= 77:
         assert fallbacks >= 1  # the adversary does reach the heap fallback here
+
+
+def test_wave_model_matches_libstdcxx():
+    """The one-wave-per-row top-k (tools/wave_topk_model.py, step for step the HIP
+    mxa_topk_wave.hpp: rank-form partition with slot tables, pending-range stack,
+    boundary bits, stable rank per final segment) against libstdc++ (oracle/topk_ref.cpp)
+    on ex_pred rows, small-integer tie rows and antiqsort depth-limit rows."""
+    from tools.wave_topk_model import wave_topk
+    rng = np.random.default_rng(7)
+    q = rng.standard_normal((1, 64, 64), dtype=np.float32)
+    kk = rng.standard_normal((1, 197, 64), dtype=np.float32)
+    aq, ak = O.approx_operands(q, kk, "ex_pred")
+    pred = O.exact_matmul_f32(aq, np.swapaxes(ak, -1, -2)).reshape(-1, 197)
+    for k in (20, 30):
+        _, want = O.topk(pred, k)
+        for r in range(len(pred)):
+            np.testing.assert_array_equal(wave_topk(pred[r], k), want[r])
+    for n, k in [(256, 154), (100, 99), (300, 17), (512, 300), (5, 3), (17, 17), (40, 1), (64, 2)]:
+        for _ in range(6):
+            v = rng.integers(0, 4, size=n).astype(np.float32)
+            np.testing.assert_array_equal(wave_topk(v, k), O.topk(v[None], k)[1][0])
+        a = O.antiqsort_row(n, k)
+        np.testing.assert_array_equal(wave_topk(a, k), O.topk(a[None], k)[1][0])
