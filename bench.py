@@ -256,9 +256,9 @@ def _unique_kernel(d, stage):
 
 
 def stage_of_kernel(name):
-    if "select_kernel" in name:
+    if "select_kernel" in name or "select_wave_kernel" in name:
         return "select"
-    if "finish_kernel" in name or "dense_rows_kernel" in name:
+    if "finish_kernel" in name or "finish16_kernel" in name or "dense_rows_kernel" in name:
         return "finish"
     if "attn_prep_kernel" in name:
         return "prep"

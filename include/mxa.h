@@ -118,7 +118,8 @@ int mxa_approx_values(const void* x, void* out, int64_t rows, int32_t d, int64_t
  * order (aten TopKImpl.h:45-86 -> libstdc++ nth_element + sort / partial_sort),
  * as called at workloads/deit/scripts/main.py:123, workloads/DiT/models.py:194,
  * workloads/PixArt/models/MX_transformer_block.py:678, :825.
- * rows x n float32 with leading dim ld; n <= 512.  out_vals nullable.
+ * rows x n with leading dim ld; n <= 1024 (PixArt 512x512 self-attention rows:
+ * MX_transformer_block.py:648-717, 1,024 tokens).  out_vals nullable.
  * out_mask (nullable): the prune mask zeros.scatter_(-1, idx, 1) of the callers
  * (deit main.py:147-148; examples/deit/top_k.py:16-42) as rows x ceil(n/32)
  * words, bit j%32 of word j/32 set iff j is kept.  vals / out_vals: dtype (MXA_DT_*).

@@ -20,7 +20,7 @@ UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", ""
          ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
-           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
+           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_finish16.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
            "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -30,10 +30,14 @@ OBJDIR = os.path.join(HERE, "build")  # per-unit objects + dependency files (git
 
 
 def _stale(lib=LIB):
+    """The library is stale when it is missing or older than any source / header of
+    csrc/ or include/ (globbed, so a new header counts without being listed) or this file."""
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    import glob
+    deps = glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.hpp"))
+    deps += glob.glob(os.path.join(HERE, "..", "include", "*.h")) + [os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

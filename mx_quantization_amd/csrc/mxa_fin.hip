@@ -3,6 +3,7 @@
 #include <algorithm>
 
 #include "mxa_finish.hpp"
+#include "mxa_finish16.hpp"
 #include "mxa_launch.hpp"
 
 namespace mxa {
@@ -115,7 +116,93 @@ static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
   if (ks <= 16) return launch_finish_ks<NB, 16, false>(ra, BH, stream);
   return launch_finish_ks<NB, 32, false>(ra, BH, stream);
 }
+// ---- finishing kernel, 16-row tiles (mxa_finish16.hpp) --------------------------------
+#ifndef MXA_FIN16  // 1: 16-row tiles, V^T from memory (default); 0: 32-row tiles (A/B builds)
+#define MXA_FIN16 1
+#endif
+// waves per workgroup: the fewest sequential tile rounds per CU -- workgroups per CU over
+// the concurrency the LDS and the kernel's registers allow, times each workgroup's rounds
+// over its tiles (a head's tiles round-robin over the waves: the K table staged once)
+static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, int* waves, int* rows_per_wg) {
+  const int tiles = (ra.N + kFin16 - 1) / kFin16;
+  const bool xo = ra.xo_codes != nullptr;
+  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, xo).total; };
+  if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
+  int chunks = 1;
+  while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
+  const int tpc = (tiles + chunks - 1) / chunks;
+  const int64_t wgs_per_cu = ((int64_t)BH * chunks + 255) / 256;
+  const int wave_cap = 4 * std::max(1, std::min(8, regs_waves_per_simd));
+  int w = 1;
+  int64_t best = -1;
+  for (int c = 1; c <= std::min(8, tpc); ++c) {
+    const size_t t = lds(c);
+    if (t > 160 * 1024) break;
+    const int64_t conc = std::max<int64_t>(1, std::min<int64_t>(160 * 1024 / t, wave_cap / c));
+    const int64_t score = (wgs_per_cu + conc - 1) / conc * ((tpc + c - 1) / c);
+    if (best < 0 || score < best) best = score, w = c;
+  }
+  *waves = w;
+  *rows_per_wg = kFin16 * ((tiles + chunks - 1) / chunks);
+  return MXA_OK;
+}
+template <int NB, int KS, int LPR, bool XDT, bool XO>
+static int launch_finish16_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
+  Rows2Args ra = ra0;
+  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, LPR, XDT, XO>);
+  static int regs_wps = 0;  // waves per SIMD the kernel's registers allow (per process: one device kind)
+  if (!regs_wps) {
+    hipFuncAttributes fa{};
+    regs_wps = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
+  }
+  int rc = finish16_plan(ra, BH, regs_wps, &ra.waves, &ra.rows_per_wg);
+  if (rc) return rc;
+  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, XO).total;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  hipLaunchKernelGGL((finish16_kernel<NB, KS, LPR, XDT, XO>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NB, int KS, int LPR>
+static int launch_finish16_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
+  if (ra.xo_codes) {  // output MX codes for the proj Linear: float32, D % 32 == 0
+    if (ra.s_dt != kF32 || ra.in_dt != kF32 || ra.D % 32) return MXA_ERR_UNSUPPORTED;
+    return launch_finish16_xdt<NB, KS, LPR, false, true>(ra, BH, stream);
+  }
+  if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish16_xdt<NB, KS, LPR, true, false>(ra, BH, stream);
+  return launch_finish16_xdt<NB, KS, LPR, false, false>(ra, BH, stream);
+}
+template <int NB>
+static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
+  const int k = ra.k_top;
+  if (k <= 64) {  // four lanes per row: slots ceil(k / 4)
+    const int ks = (k + 3) / 4;
+    if (ks <= 2) return launch_finish16_ks<NB, 2, 4>(ra, BH, stream);
+    if (ks <= 4) return launch_finish16_ks<NB, 4, 4>(ra, BH, stream);
+    if (ks <= 8) return launch_finish16_ks<NB, 8, 4>(ra, BH, stream);
+    if (ks <= 12) return launch_finish16_ks<NB, 12, 4>(ra, BH, stream);
+    return launch_finish16_ks<NB, 16, 4>(ra, BH, stream);
+  }
+  return MXA_ERR_UNSUPPORTED;  // k > 64: the 32-row kernel (launch_finish)
+}
+
 static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k
+  // (DiT's 154): the 32-row kernel (measured: DiT-XL/2 0.35 ms there vs 0.39 with
+  // 16-row tiles of sixteen lanes per row)
+  if (MXA_FIN16 && ra.k_top <= 64) {
+    if (plan) {
+      int w, r;
+      return finish16_plan(ra, BH, 2, &w, &r);
+    }
+    switch (ra.nbd) {
+      case 1: return launch_finish16_nb<1>(ra, BH, stream);
+      case 2: return launch_finish16_nb<2>(ra, BH, stream);
+      case 3: return launch_finish16_nb<3>(ra, BH, stream);
+      default: return launch_finish16_nb<4>(ra, BH, stream);
+    }
+  }
   if (plan) {
     int w, r;
     return finish_plan(ra, BH, &w, &r);

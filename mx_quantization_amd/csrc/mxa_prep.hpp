@@ -29,6 +29,18 @@ __device__ __forceinline__ uint32_t blk_reduce(uint32_t v, Op op) {
   return v;
 }
 
+// where the EPL codes of lane `sub` of a block go: row-major (row * dpad + c0), or with
+// a.mfma_rows (EPL >= 8) the MX GEMM's MFMA-ready A layout -- per 32-row block and
+// K-block, 64 lanes x 16 B, lane (row & 31) + 32 h holding elements 16 h .. 16 h + 15
+template <int EPL>
+__device__ __forceinline__ int64_t mfma_base(const RowsPrepArgs& a, int64_t row, int blk, int sub, int c0) {
+  if (EPL >= 8 && a.mfma_rows) {
+    const int e0 = EPL * sub;  // first element of the lane within the block
+    return (((row >> 5) * a.nb + blk) * 64 + (row & 31) + 32 * (e0 >> 4)) * 16 + (e0 & 15);
+  }
+  return row * a.dpad + c0;
+}
+
 // One 32-element block of a row, 32/EPL lanes x EPL elements (lane sub of its group,
 // c0 = 32 blk + EPL sub): MXINT8 codes, block exponent, approximator operand and sign
 // word into the RowsPrepArgs outputs (row `row`, block `blk`).  The lanes of a group
@@ -111,8 +123,7 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       break;
   }
   if (valid) {
-    const int64_t base = (EPL == 16 && a.mfma_rows) ? (((row >> 5) * a.nb + blk) * 64 + (row & 31) + 32 * sub) * 16
-                                                    : row * a.dpad + c0;
+    const int64_t base = mfma_base<EPL>(a, row, blk, sub, c0);
     uint32_t pc[EPL / 4], po[EPL / 4], pz[EPL / 4];
 #pragma unroll
     for (int w = 0; w < EPL / 4; ++w) {
@@ -128,6 +139,10 @@ __device__ __forceinline__ void rows_prep_block(const RowsPrepArgs& a, int64_t r
       if (a.codes) *reinterpret_cast<uint4*>(a.codes + base) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
       if (a.op) *reinterpret_cast<uint4*>(a.op + base) = make_uint4(po[0], po[1], po[2], po[3]);
       if (a.zind) *reinterpret_cast<uint4*>(a.zind + base) = make_uint4(pz[0], pz[1], pz[2], pz[3]);
+    } else if constexpr (EPL == 8) {
+      if (a.codes) *reinterpret_cast<uint2*>(a.codes + base) = make_uint2(pc[0], pc[1]);
+      if (a.op) *reinterpret_cast<uint2*>(a.op + base) = make_uint2(po[0], po[1]);
+      if (a.zind) *reinterpret_cast<uint2*>(a.zind + base) = make_uint2(pz[0], pz[1]);
     } else {
       if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc[0];
       if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = po[0];
@@ -197,12 +212,15 @@ __device__ __forceinline__ void rows_prep_block_plain(const RowsPrepArgs& a, int
     for (int w = 0; w < EPL / 4; ++w)
       pc[w] = (uint32_t)(code[4 * w] & 0xFF) | (uint32_t)(code[4 * w + 1] & 0xFF) << 8 |
               (uint32_t)(code[4 * w + 2] & 0xFF) << 16 | (uint32_t)code[4 * w + 3] << 24;
-    const int64_t base = (EPL == 16 && a.mfma_rows) ? (((row >> 5) * a.nb + blk) * 64 + (row & 31) + 32 * sub) * 16
-                                                    : row * a.dpad + c0;
+    const int64_t base = mfma_base<EPL>(a, row, blk, sub, c0);
     if constexpr (EPL == 16) {
       const uint4 v = make_uint4(pc[0], pc[1], pc[2], pc[3]);
       if (a.codes) *reinterpret_cast<uint4*>(a.codes + base) = v;
       if (a.op) *reinterpret_cast<uint4*>(a.op + base) = v;  // MXA_OP_MXINT8 (SIGN has none)
+    } else if constexpr (EPL == 8) {
+      const uint2 v = make_uint2(pc[0], pc[1]);
+      if (a.codes) *reinterpret_cast<uint2*>(a.codes + base) = v;
+      if (a.op) *reinterpret_cast<uint2*>(a.op + base) = v;
     } else {
       if (a.codes) *reinterpret_cast<uint32_t*>(a.codes + base) = pc[0];
       if (a.op) *reinterpret_cast<uint32_t*>(a.op + base) = pc[0];

@@ -47,7 +47,7 @@ static int launch_select_wave(const Rows2Args& ra0, int BH, hipStream_t stream, 
 }
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (MXA_SEL_WAVE) return launch_select_wave<NP, MODE>(ra, BH, stream, plan);
+  if constexpr (MXA_SEL_WAVE) return launch_select_wave<NP, MODE>(ra, BH, stream, plan);
   if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
   return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
 }
@@ -115,7 +115,7 @@ extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, i
                         void* out_vals, uint32_t* out_mask, int32_t dtype, hipStream_t stream) {
   if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
   if (dtype != kF32 && dtype != kF16 && dtype != kBF16) return MXA_ERR_ARG;
-  if (n > 512) return MXA_ERR_UNSUPPORTED;
+  if (n > kWMaxN) return MXA_ERR_UNSUPPORTED;
   if (rows == 0) return MXA_OK;
   if (k == 0) {
     if (out_mask) return hipMemsetAsync(out_mask, 0, (size_t)rows * ((n + 31) / 32) * 4, stream) == hipSuccess
@@ -123,10 +123,12 @@ extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, i
     return MXA_OK;
   }
   const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
-  if (MXA_SEL_WAVE) {
-    if (n <= 128) return launch_topk_wave<128>(ga, stream);
+  // rows of 513..1024 (PixArt 512x512 self-attention): one wave per row (mxa_topk_wave.hpp);
+  // shorter rows: four rows per wave (mxa_topk_grp.hpp, measured faster)
+  if (n > 512 || MXA_SEL_WAVE) {
     if (n <= 256) return launch_topk_wave<256>(ga, stream);
-    return launch_topk_wave<512>(ga, stream);
+    if (n <= 512) return launch_topk_wave<512>(ga, stream);
+    return launch_topk_wave<1024>(ga, stream);
   }
   const unsigned grid = (unsigned)((rows + 15) / 16);
   if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);

@@ -36,8 +36,11 @@ namespace mxa {
 #ifndef MXA_SELW_OCC
 #define MXA_SELW_OCC 8
 #endif
-#ifndef MXA_SEL_WAVE  // 1: one wave per query row (select_wave_kernel); 0: four rows per wave (A/B builds)
-#define MXA_SEL_WAVE 1
+// 1: the selection kernel with one wave per query row (select_wave_kernel) -- a tools
+// A/B build; measured slower than four rows per wave (DeiT-base 1.15 vs 0.80 ms: its
+// per-row scalar bookkeeping costs as much issue time as the vector work it saves)
+#ifndef MXA_SEL_WAVE
+#define MXA_SEL_WAVE 0
 #endif
 #ifndef MXA_SEL_SHORT_T
 #define MXA_SEL_SHORT_T 224
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(64 * kSelWaveW) __attribute__((amdgpu_waves_per_eu(
   const int wave = (int)(threadIdx.x >> 6);
   const uint32_t lane0 = threadIdx.x & 63;
   const int bh = blockIdx.x;
-  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst;
   const int b_ = bh / a.H, h_ = bh % a.H;
   const SelLds L = sel_lds(MODE, T, D, kst, nbd);
   int8_t* tcd = reinterpret_cast<int8_t*>(smem + L.cd);
@@ -539,6 +542,10 @@ __global__ __launch_bounds__(64 * kSelWaveW) __attribute__((amdgpu_waves_per_eu(
           nbk[b] = min(32, D - 32 * b);
         }
         float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
+        // the common case branch-free (exponent spread <= 23, smallest >= -100: the exact
+        // int32 sum, one rounding); rows with any other key (NaN blocks, wide spreads)
+        // get a second pass over the flagged keys with the exact fp64 sum
+        uint64_t anyslow = 0;
         for (int j = (int)lane; j < T; j += 64) {
           const int16_t* kex = tex + j * NBD;
           const uint32_t* ksg = tsg + j * NBD;
@@ -554,21 +561,30 @@ __global__ __launch_bounds__(64 * kSelWaveW) __attribute__((amdgpu_waves_per_eu(
             emin = min(emin, e[b]);
             emax = max(emax, e[b]);
           }
-          float v;
-          uint32_t key;
-          if (emax - emin <= 23 && emin >= -100) {
-            int sum = 0;
+          int sum = 0;
 #pragma unroll
-            for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
-            v = ldexpf((float)sum, emin);
-            const uint32_t u = __float_as_uint(v);
-            key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
-          } else {
-            v = expred_score<NBD>(sq, eq, kex, ksg, D);
-            key = order_key(v);
-          }
+          for (int b = 0; b < NBD; ++b) sum += m[b] << ((e[b] - emin) & 31);
+          const float v = ldexpf((float)sum, emin);
+          const uint32_t u = __float_as_uint(v);
+          anyslow |= w_ballot(!(emax - emin <= 23 && emin >= -100));
           if (prow) prow[j] = v;
-          g.A[j] = pack_ki(key, (uint32_t)j);
+          g.A[j] = pack_ki(u ^ ((uint32_t)((int)u >> 31) | 0x80000000u), (uint32_t)j);
+        }
+        if (anyslow) {
+          for (int j = (int)lane; j < T; j += 64) {
+            const int16_t* kex = tex + j * NBD;
+            int emin = 1 << 20, emax = -(1 << 20);
+#pragma unroll
+            for (int b = 0; b < NBD; ++b) {
+              emin = min(emin, eqr[b] + (int)kex[b]);
+              emax = max(emax, eqr[b] + (int)kex[b]);
+            }
+            if (!(emax - emin <= 23 && emin >= -100)) {
+              const float v = expred_score<NBD>(sq, eq, kex, tsg + j * NBD, D);
+              if (prow) prow[j] = v;
+              g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+            }
+          }
         }
       };
       switch (nbd) {
@@ -696,7 +712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
 // one wave per row (mxa_topk_wave.hpp): waves of a 256-thread workgroup take rows
 // 4 blockIdx.x + wave
 template <int NP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : 4, 8))) void topk_wave_kernel(GrpTopkArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : NP <= 512 ? 4 : 2, 8))) void topk_wave_kernel(GrpTopkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = (int)(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;

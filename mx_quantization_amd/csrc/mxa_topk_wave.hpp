@@ -44,15 +44,16 @@ typedef __attribute__((address_space(3))) uint16_t wl16;
 // per-row LDS: mirror A[n + 64] (order key << 32 | index; the window of a step may read
 // up to 63 positions past the row), slot tables SL[n], SR[n] (u16 positions), 16-B aligned
 __host__ __device__ constexpr int wrow_mirror(int n) { return n + 64; }
+constexpr int kWMaxN = 1024;  // longest row (positions < 1024: 10-bit fields, 32 boundary words)
 __host__ __device__ constexpr size_t wrow_bytes(int n) {
-  return (size_t)8 * wrow_mirror(n) + (((size_t)4 * n + 15) & ~(size_t)15) + 64 + 512;
+  return (size_t)8 * wrow_mirror(n) + (((size_t)4 * n + 15) & ~(size_t)15) + 128 + 512;
 }
 
 struct WRow {
   lu64* A;
   wl16* SL;
   wl16* SR;
-  wl32* BW;  // final-segment boundaries of the sort phase, one bit per position (<= 512)
+  wl32* BW;  // final-segment boundaries of the sort phase, one bit per position (32 words)
   lu64* TR;  // trash: one 8-B slot per lane for the stores of lanes with nothing to store
 };
 __device__ __forceinline__ WRow carve_wrow(unsigned char* base, int n) {
@@ -61,7 +62,7 @@ __device__ __forceinline__ WRow carve_wrow(unsigned char* base, int n) {
   g.SL = (wl16*)(base + (size_t)8 * wrow_mirror(n));
   g.SR = g.SL + n;
   g.BW = (wl32*)(base + (size_t)8 * wrow_mirror(n) + (((size_t)4 * n + 15) & ~(size_t)15));
-  g.TR = (lu64*)(g.BW + 16);
+  g.TR = (lu64*)(g.BW + 32);
   return g;
 }
 
@@ -118,13 +119,17 @@ __device__ __forceinline__ int w_part_e(const WRow& g, int f, int l, uint32_t la
   const uint64_t mb = 1ull << ((m - f) & 63);
   const bool mL = kf <= p, mR = kf >= p;
   // pass 1: the right stops' count (position f is never a stop)
-  uint64_t Rm[E];
+  auto rmask = [&](int e) {
+    const uint64_t sel = e == em ? mb : 0ull;  // scalar selects, no branch
+    return ((w_ballot(K[e] >= p) & w_rng(e == 0 ? 1 : 0, l - f - 64 * e)) & ~sel) | (mR ? sel : 0ull);
+  };
+  constexpr bool kKeepR = E <= 4;  // wider windows recompute the masks (SGPRs are the budget)
+  uint64_t Rm[kKeepR ? E : 1];
   int totR = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const uint64_t sel = e == em ? mb : 0ull;  // scalar selects, no branch
-    const uint64_t r = ((w_ballot(K[e] >= p) & w_rng(e == 0 ? 1 : 0, l - f - 64 * e)) & ~sel) | (mR ? sel : 0ull);
-    Rm[e] = r;
+    const uint64_t r = rmask(e);
+    if (kKeepR) Rm[e] = r;
     totR += __popcll(r);
   }
   // pass 2: inclusive prefix counts, the slot tables, the cut and the swap count.
@@ -139,7 +144,7 @@ __device__ __forceinline__ int w_part_e(const WRow& g, int f, int l, uint32_t la
     const uint64_t rng = w_rng(e == 0 ? 1 : 0, l - f - 64 * e);
     const uint64_t sel = e == em ? mb : 0ull;
     const uint64_t Lm = ((w_ballot(K[e] <= p) & rng) & ~sel) | (mL ? sel : 0ull);
-    const uint64_t R = Rm[e];
+    const uint64_t R = kKeepR ? Rm[kKeepR ? e : 0] : rmask(e);
     const uint32_t PLi = w_mbcnt(Lm >> 1, (uint32_t)baseL + (uint32_t)(Lm & 1));
     const uint32_t PRi = w_mbcnt(R >> 1, (uint32_t)baseR + (uint32_t)(R & 1));
     const uint16_t z = (uint16_t)(f + 64 * e + (int)lane);
@@ -168,8 +173,10 @@ __device__ __forceinline__ int w_partition(const WRow& g, int f, int l, uint32_t
   if (EW <= 1 || E == 2) return w_part_e<EW < 2 ? 1 : 2>(g, f, l, lane);
   if (EW <= 2 || E == 3) return w_part_e<EW < 3 ? 1 : 3>(g, f, l, lane);
   if (EW <= 3 || E == 4) return w_part_e<EW < 4 ? 1 : 4>(g, f, l, lane);
-  if (E <= 6) return w_part_e<EW < 6 ? 1 : 6>(g, f, l, lane);
-  return w_part_e<EW < 8 ? 1 : 8>(g, f, l, lane);
+  if (EW <= 4 || E <= 6) return w_part_e<EW < 6 ? 1 : 6>(g, f, l, lane);
+  if (EW <= 6 || E <= 8) return w_part_e<EW < 8 ? 1 : 8>(g, f, l, lane);
+  if (EW <= 8 || E <= 12) return w_part_e<EW < 12 ? 1 : 12>(g, f, l, lane);
+  return w_part_e<EW < 16 ? 1 : 16>(g, f, l, lane);
 }
 
 // boundary bit at position c (ds_or: no return value waited on)
@@ -224,12 +231,12 @@ __device__ __forceinline__ void wave_topk(const WRow& g, int n, int k) {
   // disjoint ranges are independent, so the pending ranges go on a stack (one per lane
   // of a VGPR) in any order; every cut starts a final segment (boundary bits BW, plus 0
   // and m).
-  if ((int)lane < 16) g.BW[lane] = lane == 0 ? 1u : 0u;
+  if ((int)lane < 32) g.BW[lane] = lane == 0 ? 1u : 0u;
   wave_lds_sync();
   if (lane == 0) w_mark(g, m);
   int maxlen = 0;  // longest final segment that is not heap-sorted
   {
-    uint32_t stk = 0;  // lane s: pending range s (f | l << 10 | d << 20)
+    uint32_t stk = 0;  // lane s: pending range s (f | l << 11 | d << 22)
     int sp = 0;
     int f = 0, l = m, d = 2 * ilog2(m);
     while (true) {
@@ -237,7 +244,7 @@ __device__ __forceinline__ void wave_topk(const WRow& g, int n, int k) {
         --d;
         const int cut = w_partition<EW>(g, f, l, lane);
         if (lane == 0) w_mark(g, cut);
-        stk = lane == (uint32_t)sp ? (uint32_t)cut | ((uint32_t)l << 10) | ((uint32_t)d << 20) : stk;
+        stk = lane == (uint32_t)sp ? (uint32_t)cut | ((uint32_t)l << 11) | ((uint32_t)d << 22) : stk;
         ++sp;
         l = cut;
       }
@@ -254,9 +261,9 @@ __device__ __forceinline__ void wave_topk(const WRow& g, int n, int k) {
       if (sp == 0) break;
       --sp;
       const uint32_t s = w_readlane(stk, sp);
-      f = (int)(s & 1023u);
-      l = (int)((s >> 10) & 1023u);
-      d = (int)(s >> 20);
+      f = (int)(s & 2047u);
+      l = (int)((s >> 11) & 2047u);
+      d = (int)(s >> 22);
     }
   }
   if (maxlen < 2) return;  // every segment a singleton or heap-sorted
@@ -278,7 +285,7 @@ __device__ __forceinline__ void wave_topk(const WRow& g, int n, int k) {
       const uint64_t x = g.A[zc];
       X[e] = x;
       const int w = zc >> 5, o = zc & 31;
-      const uint32_t b0 = w > 0 ? g.BW[w - 1] : 0u, b1 = g.BW[w], b2 = w < 15 ? g.BW[w + 1] : 0u;
+      const uint32_t b0 = w > 0 ? g.BW[w - 1] : 0u, b1 = g.BW[w], b2 = w < 31 ? g.BW[w + 1] : 0u;
       // s: highest set bit at or below z (bit 32 + o of b0:b1:b2 is z)
       const uint64_t lowin = ((uint64_t)b1 << 32 | b0) & (~0ull >> (31 - o));  // bits <= 32 + o
       const int s = zc - (32 + o - (63 - (int)__clzll(lowin)));

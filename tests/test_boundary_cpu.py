@@ -37,7 +37,7 @@ def test_status_strings_and_arg_errors():
     assert lib.mxa_quantize_mx(None, None, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, 0, None) == -1
     assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 5, 8, 0, 0, 0, 0, None) == -2  # fp formats
     assert lib.mxa_quantize_mx(1, 1, None, None, 1, 1, 1, 32, 8, 8, 0, 0, 0, 7, None) == -1  # bad dtype
-    assert lib.mxa_topk(1, 1, 600, 600, 3, 1, None, None, 0, None) == -2  # n > 512
+    assert lib.mxa_topk(1, 1, 1100, 1100, 3, 1, None, None, 0, None) == -2  # n > 1024
     assert lib.mxa_topk(1, 1, 10, 10, 11, 1, None, None, 0, None) == -1  # k > n
     assert lib.mxa_topk(1, 1, 10, 10, 3, 1, None, None, 5, None) == -1  # bad dtype
     p = N.AttnParams()
@@ -214,3 +214,40 @@ def test_exact_topk_bind_cpu():
     assert torch.equal(r.indices, w.indices) and torch.equal(r.values, w.values)
     M.unbind_exact_topk(mod)
     assert mod.torch is torch
+
+
+def test_committed_profiles_name_current_kernels():
+    """The bench line's roofline.traffic / limiter come from the committed profiles of
+    bench.PROFILE_TAG (profiles/<tag>_{rocprof,traffic,pmc}_*): every kernel they name
+    must be a kernel of the current library, and each main-line profile must hold the
+    current selection kernel family -- so a kernel change without new profiles fails."""
+    import glob
+    import json
+    import subprocess
+
+    import bench
+    lib = os.path.join(ROOT, "mx_quantization_amd", "libmxa.so")
+    if not os.path.exists(lib):
+        pytest.skip("libmxa.so not built")
+    syms = subprocess.run(["nm", "-C", lib], capture_output=True, text=True, check=True).stdout
+    kernels = {ln.split(" ", 2)[2] for ln in syms.splitlines() if " mxa::" in ln and ln.count(" ") >= 2}
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"{bench.PROFILE_TAG}_*")))
+    assert files, f"no committed profiles for PROFILE_TAG {bench.PROFILE_TAG}"
+    named = set()
+    for f in files:
+        if f.endswith(".csv"):
+            import csv
+            with open(f) as fh:
+                named |= {r["Name"] for r in csv.DictReader(fh) if "mxa::" in r["Name"]}
+        elif "_traffic_" in f and f.endswith(".json"):
+            with open(f) as fh:
+                named |= set(json.load(fh)["kernels"])
+        elif "_pmc_" in f and f.endswith(".json"):
+            with open(f) as fh:
+                named |= {k for k in json.load(fh) if "mxa::" in k}
+    missing = sorted(n for n in named if n not in kernels)
+    assert not missing, f"profiles name kernels the library does not have: {missing[:4]}"
+    for cfg in ("deit_base", "dit_xl2"):
+        with open(os.path.join(ROOT, "profiles", f"{bench.PROFILE_TAG}_traffic_{cfg}.json")) as fh:
+            sel = [k for k in json.load(fh)["kernels"] if bench.stage_of_kernel(k) == "select"]
+        assert len(sel) == 1 and sel[0] in kernels, sel

@@ -185,6 +185,23 @@ def test_topk_many_tie_rows(M, n):
         same(host(idx), want, f"n{n} k{k}")
 
 
+@pytest.mark.parametrize("n,k", [(1024, 20), (1024, 154), (700, 300), (1000, 999)])
+def test_topk_rows_up_to_1024(M, n, k):
+    """Rows longer than 512 (PixArt 512x512 self-attention: 1,024 tokens,
+    MX_transformer_block.py:648-717, topk at :678): ex_pred-like tie rows, small
+    alphabets and an antiqsort depth-limit row, against libstdc++."""
+    rng = np.random.default_rng(n + k)
+    q = rng.standard_normal((1, 8, 72), dtype=np.float32)
+    kk = rng.standard_normal((1, n, 72), dtype=np.float32)
+    aq, ak = O.approx_operands(q, kk, "ex_pred")
+    rows = np.concatenate([O.exact_matmul_f32(aq, np.swapaxes(ak, -1, -2)).reshape(-1, n),
+                           rng.integers(-3, 4, (8, n)).astype(np.float32), O.antiqsort_row(n, k)[None]])
+    _, want = O.topk(rows, k)
+    _, idx, words = M.topk(dev(rows), k, return_mask=True)
+    same(host(idx), want, f"n{n} k{k}")
+    same(host(M.unpack_mask(words, n)), O.prune_mask(want, n), f"n{n} k{k} mask")
+
+
 # ------------------------------------------------------------------ approximators
 @pytest.mark.parametrize("mode", ["ex_pred", "partial_Q", "partial_K", "MXINT4", "two_step_leading_ones", "true_ex"])
 def test_approximator_operands(M, mode):

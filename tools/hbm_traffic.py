@@ -25,9 +25,9 @@ import sys
 
 
 def stage_of(kernel):
-    if "select_kernel" in kernel:
+    if "select_kernel" in kernel or "select_wave_kernel" in kernel:
         return "select"
-    if "finish_kernel" in kernel or "dense_rows_kernel" in kernel:
+    if "finish_kernel" in kernel or "finish16_kernel" in kernel or "dense_rows_kernel" in kernel:
         return "finish"
     if "attn_prep_kernel" in kernel:
         return "prep"
