@@ -45,7 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MXINT8 attn fwd tokens/s/GPU (DeiT-base, DiT-XL/2); top-k idx bit-match"
-PROFILE_TAG = "r03v3"  # the profiling session whose committed PMC files the bench line cites
+PROFILE_TAG = "r04v2"  # the profiling session whose committed PMC files the bench line cites
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: dense I8 MFMA = 2x BF16 (~2.5 PF) per clock
 
@@ -371,12 +371,14 @@ def run_config(c, images, steps, warmup, device, world, prof=None):
                     "bytes": bytes_qa(cb), "ms": qa_ms, "achieved": qa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": qa_gbs / HBM_PEAK_GBS},
         "mfma": {"what": "SURVEY §8d Ops_gemm (dense QK^T + PV int8 ops) over the finishing kernel's time; "
-                         "that kernel runs P.V on v_mfma_i32_32x32x32_i8 (one per 32-key MX block and 32 "
-                         "output columns of a 32-row P tile) and the kept keys' QK^T with v_dot4, so this "
+                         "that kernel runs P.V on int8 MFMA (one per 32-key MX block and 16 / 32 output "
+                         "columns of a 16- / 32-row P tile) and the kept keys' QK^T with v_dot4, so this "
                          "is the dense-equivalent rate",
                  "ops": ops_gemm(cb), "ms": stages["finish"], "achieved": mf_tops, "peak": I8_PEAK_TOPS,
                  "unit": "TOPS", "frac": mf_tops / I8_PEAK_TOPS,
-                 "engine": "P.V: v_mfma_i32_32x32x32_i8; kept-key QK^T: v_dot4"},
+                 # mxa_fin.hip launch_finish: 16-row tiles for k <= 64, else 32-row tiles
+                 "engine": ("P.V: v_mfma_i32_16x16x32_i8" if cb["k"] <= 64 else "P.V: v_mfma_i32_32x32x32_i8")
+                           + "; kept-key QK^T: v_dot4"},
     }
     e2e = {"fused_min_bytes": fused_min_bytes(cb),
            "achieved_GBs": fused_min_bytes(cb) / (sum(stages.values()) * 1e-3) / 1e9}

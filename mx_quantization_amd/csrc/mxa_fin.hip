@@ -6,6 +6,12 @@
 #include "mxa_finish16.hpp"
 #include "mxa_launch.hpp"
 
+// 1: the finishing kernel on 16-row tiles for k <= 64 (mxa_finish16.hpp; default); 0: the
+// 32-row kernel for every k (A/B builds)
+#ifndef MXA_FIN16
+#define MXA_FIN16 1
+#endif
+
 namespace mxa {
 
 // ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
@@ -117,16 +123,12 @@ static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
   return launch_finish_ks<NB, 32, false>(ra, BH, stream);
 }
 // ---- finishing kernel, 16-row tiles (mxa_finish16.hpp) --------------------------------
-#ifndef MXA_FIN16  // 1: 16-row tiles, V^T from memory (default); 0: 32-row tiles (A/B builds)
-#define MXA_FIN16 1
-#endif
 // waves per workgroup: the fewest sequential tile rounds per CU -- workgroups per CU over
 // the concurrency the LDS and the kernel's registers allow, times each workgroup's rounds
 // over its tiles (a head's tiles round-robin over the waves: the K table staged once)
 static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, int* waves, int* rows_per_wg) {
   const int tiles = (ra.N + kFin16 - 1) / kFin16;
-  const bool xo = ra.xo_codes != nullptr;
-  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, xo).total; };
+  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w).total; };
   if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   int chunks = 1;
   while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
@@ -146,10 +148,10 @@ static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, i
   *rows_per_wg = kFin16 * ((tiles + chunks - 1) / chunks);
   return MXA_OK;
 }
-template <int NB, int KS, int LPR, bool XDT, bool XO>
+template <int NB, int KS, int LPR, bool XDT>
 static int launch_finish16_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
-  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, LPR, XDT, XO>);
+  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, LPR, XDT>);
   static int regs_wps = 0;  // waves per SIMD the kernel's registers allow (per process: one device kind)
   if (!regs_wps) {
     hipFuncAttributes fa{};
@@ -157,21 +159,18 @@ static int launch_finish16_xdt(const Rows2Args& ra0, int BH, hipStream_t stream)
   }
   int rc = finish16_plan(ra, BH, regs_wps, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
-  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, XO).total;
+  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish16_kernel<NB, KS, LPR, XDT, XO>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
+  hipLaunchKernelGGL((finish16_kernel<NB, KS, LPR, XDT>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 template <int NB, int KS, int LPR>
 static int launch_finish16_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
-  if (ra.xo_codes) {  // output MX codes for the proj Linear: float32, D % 32 == 0
-    if (ra.s_dt != kF32 || ra.in_dt != kF32 || ra.D % 32) return MXA_ERR_UNSUPPORTED;
-    return launch_finish16_xdt<NB, KS, LPR, false, true>(ra, BH, stream);
-  }
-  if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish16_xdt<NB, KS, LPR, true, false>(ra, BH, stream);
-  return launch_finish16_xdt<NB, KS, LPR, false, false>(ra, BH, stream);
+  if (ra.xo_codes) return MXA_ERR_UNSUPPORTED;  // the proj's input codes: the 32-row kernel
+  if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish16_xdt<NB, KS, LPR, true>(ra, BH, stream);
+  return launch_finish16_xdt<NB, KS, LPR, false>(ra, BH, stream);
 }
 template <int NB>
 static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
@@ -191,7 +190,10 @@ static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool p
   // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k
   // (DiT's 154): the 32-row kernel (measured: DiT-XL/2 0.35 ms there vs 0.39 with
   // 16-row tiles of sixteen lanes per row)
-  if (MXA_FIN16 && ra.k_top <= 64) {
+  // The proj's MX input codes (XO) stay on the 32-row kernel: its 32 x 32 output blocks are
+  // whole MX blocks of the output rows (measured: 0.264 ms at DeiT-base against 0.308 ms
+  // for 16-row tiles, whose 16 x 32 blocks take twice the transposes and syncs per row).
+  if (MXA_FIN16 && ra.k_top <= 64 && !ra.xo_codes) {
     if (plan) {
       int w, r;
       return finish16_plan(ra, BH, 2, &w, &r);

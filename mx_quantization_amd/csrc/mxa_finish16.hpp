@@ -22,8 +22,8 @@
 //      v_mfma_i32_16x16x32_i8 (K = 32 = one block: each block keeps its exact int32 sum),
 //      epilogue acc += C * (sP[row][b] * sV[b][d]) in fp32 (P.V is a tolerance-only
 //      product).
-//   3. the tile's output rows go out (or, XO, the proj Linear's MX input codes: every
-//      32-column block of the output row quantized from the LDS output tile).
+//   3. the tile's output rows go out.  (The proj Linear's MX input codes stay on the
+//      32-row kernel, whose 32 x 32 output blocks are whole MX blocks of the rows.)
 // Reference: microxscaling/mx/matmul.py:68-76 (MX P.V), callers
 // workloads/deit/scripts/main.py:124-152, workloads/DiT/models.py:195-225,
 // workloads/PixArt/models/MX_transformer_block.py:679-717, :826-859.
@@ -34,21 +34,23 @@ namespace mxa {
 
 constexpr int kFin16 = 16;  // query rows per MFMA tile (one wave)
 #ifndef MXA_FIN16_OCC  // waves per SIMD the register allocation aims at
-#define MXA_FIN16_OCC 3
+#define MXA_FIN16_OCC 4
 #endif
-#ifndef MXA_FIN16_VTLDS  // 1: V^T codes staged in LDS with the K table; 0: MFMA B operands from memory
-#define MXA_FIN16_VTLDS 1
+// 1: V^T codes staged in LDS with the K table; 0: the MFMA B operands straight from
+// memory (measured at DeiT-base: 0.200 ms with 4 waves per SIMD, against 0.214 ms staged
+// at 3 waves per SIMD -- the staged table and a prefetched input set cost the fourth wave)
+#ifndef MXA_FIN16_VTLDS
+#define MXA_FIN16_VTLDS 0
 #endif
 
 typedef int v4i16_ __attribute__((ext_vector_type(4)));
 
 // LDS: tables (K codes, K exponents, V block exponents), then per wave the P code tile
-// [16][vst], the P block scales sP [ntb][16] (float), the block maxima bm [16][ntb]
-// (u32), and (XO) the 16 x 32 fp32 output block being MX-quantized
+// [16][vst], the P block scales sP [ntb][16] (float), the block maxima bm [16][ntb] (u32)
 struct Fin16Lds {
-  size_t kc, ke, vt, ve, waves, per_wave, sp, bm, ot, total;
+  size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
 };
-__host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves, bool xo) {
+__host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves) {
   Fin16Lds L;
   size_t o = 0;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -63,13 +65,12 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   L.waves = o;
   L.sp = al((size_t)kFin16 * vst);
   L.bm = L.sp + al((size_t)ntb * kFin16 * 4);
-  L.ot = L.bm + al((size_t)kFin16 * ntb * 4);
-  L.per_wave = L.ot + (xo ? kFin16 * 33 * 4 : 0);
+  L.per_wave = L.bm + al((size_t)kFin16 * ntb * 4);
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
 
-template <int NB, int KS, int LPR, bool XDT, bool XO = false>
+template <int NB, int KS, int LPR, bool XDT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && KS <= 12 ? MXA_FIN16_OCC : (NB * KS <= 64 ? 3 : 2), 8))) void finish16_kernel(Rows2Args a) {
   static_assert(LPR == 4 || LPR == 16, "four or sixteen lanes per query row");
   const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   const int T = a.T, D = a.D, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
   constexpr int nbd = NB;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const Fin16Lds L = fin16_lds(T, D, kst, nbd, vst, ntb, a.waves, XO);
+  const Fin16Lds L = fin16_lds(T, D, kst, nbd, vst, ntb, a.waves);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
   int16_t* tve = reinterpret_cast<int16_t*>(smem + L.ve);
@@ -115,9 +116,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
 
   const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
   constexpr int kPasses = LPR == 4 ? 1 : kFin16 / 4;
-  // a pass's global inputs (the row's query codes / exponents and kept indices), loaded
-  // one pass ahead so that their latency hides behind the previous pass (measured: without
-  // it the waves spend half their cycles waiting on these loads)
+  // a pass's global inputs (the row's query codes / exponents and kept indices); loaded
+  // at the start of the pass -- the resident waves hide their latency (a copy loaded one
+  // pass ahead costs the registers of a resident wave)
   struct PassIn {
     uint4 qv[2 * NB];
     int qe[NB];
@@ -141,14 +142,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     }
   };
 
-  PassIn nxt;
-  if (r_beg + kFin16 * wave < r_end) load_pass(r_beg + kFin16 * wave, 0, nxt);
   for (int r0 = r_beg + kFin16 * wave; r0 < r_end; r0 += kFin16 * a.waves) {
     // ---- 1. kept scores, softmax, MX(P) into the code tile ------------------------------
     for (int pass = 0; pass < kPasses; ++pass) {
-      const PassIn cur = nxt;
-      if (pass + 1 < kPasses) load_pass(r0, pass + 1, nxt);
-      else if (r0 + kFin16 * a.waves < r_end) load_pass(r0 + kFin16 * a.waves, 0, nxt);
+      PassIn cur;
+      load_pass(r0, pass, cur);
       const int tr = LPR == 4 ? pr : 4 * pass + pr;  // row within the tile
       const int r = r0 + tr;
       const bool valid = r < r_end;
@@ -267,32 +265,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
             acc[3] = fmaf((float)c[3], s4.w * sv, acc[3]);
           }
         }
-      }
-      if constexpr (XO) {
-        // ---- 3'. two 16-column halves -> the 16 x 32 block -> MX codes of block (h D + dt) / 32
-        // of each output row (what rows_prep makes of the (B, N, C) output for the proj
-        // Linear), four lanes per row, eight elements each -------------------------------
-        float* ot = reinterpret_cast<float*>(wb + L.ot);
-        const int half = (dt >> 4) & 1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ot[(4 * kg + i) * 33 + 16 * half + ln] = round_bfloat(acc[i], a.bfloat, kRoundNearest, 1);
-        if (!half) continue;  // D % 32 == 0: the second half always follows
-        wave_lds_sync();
-        const int row = lane >> 2, sub = lane & 3, r = r0 + row;
-        float xv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = ot[row * 33 + 8 * sub + j];
-        RowsPrepArgs ro{};
-        ro.codes = a.xo_codes; ro.sT = a.xo_exps;
-        ro.dpad = a.H * D; ro.nb = a.H * nbd; ro.D = a.H * D;
-        ro.op_kind = MXA_OP_MXINT8; ro.flush = a.flush_p; ro.bfloat = a.bfloat; ro.dt = kF32;
-        ro.mfma_rows = 1;  // the MX GEMM's A layout
-        const int64_t orow = (int64_t)b_ * a.N + (r < r_end ? r : r0);
-        const int blk = h_ * nbd + (dt - 16) / 32, c0 = h_ * D + (dt - 16) + 8 * sub;
-        if (rows_prep_plain(ro)) rows_prep_block_plain<8, kF32>(ro, orow, blk, sub, c0, xv, r < r_end);
-        else rows_prep_block<8>(ro, orow, blk, sub, c0, xv, r < r_end);
-        wave_lds_sync();
-        continue;
       }
       // ---- 3. output rows (64-B segments per row) ------------------------------------
       if (dt + ln < D) {
