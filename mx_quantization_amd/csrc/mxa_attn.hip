@@ -192,9 +192,13 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   pa.pe = reinterpret_cast<const int16_t*>(wb + W.pe);
   pa.ps = reinterpret_cast<const int16_t*>(wb + W.ps);
   pa.gs = reinterpret_cast<const int16_t*>(wb + W.gs);
-  if (W.ps - W.pk >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;  // 32-bit buffer offsets
+  pa.pn = reinterpret_cast<const int16_t*>(wb + W.pn);
+  pa.pd = reinterpret_cast<const int8_t*>(wb + W.pd);
+  if (W.ps - W.pk >= ((int64_t)1 << 31) || W.total - W.pd >= ((int64_t)1 << 31))
+    return MXA_ERR_UNSUPPORTED;  // 32-bit buffer offsets
   pa.pk_bytes = (int)(W.pe - W.pk);
   pa.pe_bytes = (int)(W.ps - W.pe);
+  pa.pd_bytes = (int)(W.total - W.pd);
   pa.slow_count = reinterpret_cast<int*>(ws + L.slow);
   pa.slow_list = pa.slow_count + 1;
   pa.ntb = (pp.N + 31) / 32;

@@ -39,21 +39,50 @@ __global__ __launch_bounds__(256) void linear_pack_kernel(const int8_t* rawc, co
   pe[pc * nbk + kb] = e;
 }
 
-// per padded column: smallest finite block exponent and the spread
-__global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, int64_t pcols, int nbk, int16_t* ps) {
+// per padded column: smallest finite block exponent and the spread, the NaN flag
+__global__ __launch_bounds__(256) void linear_stats_kernel(const int16_t* pe, int64_t pcols, int nbk, int16_t* ps,
+                                                           int16_t* pn) {
   const int64_t pc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (pc >= pcols) return;
-  int lo = 1 << 20, hi = -(1 << 20);
+  int lo = 1 << 20, hi = -(1 << 20), nan = 0;
   for (int kb = 0; kb < nbk; ++kb) {
     const int e = exp_from16(pe[pc * nbk + kb]);
     if (e != kExpNaN) {
       lo = min(lo, e);
       hi = max(hi, e);
+    } else {
+      nan = 1;
     }
   }
   if (lo > hi) lo = hi = 0;
   ps[2 * pc] = (int16_t)lo;
   ps[2 * pc + 1] = (int16_t)(hi - lo);
+  pn[pc] = (int16_t)nan;
+}
+
+// one thread per (padded column, K-block): the exponent-folded digits of the MFMA-ready
+// codes (the column's two 16-B halves sit at lanes n and n + 32 of the block's 1-KB chunk)
+__global__ __launch_bounds__(256) void linear_digits_kernel(const int8_t* pk, const int16_t* pe, const int16_t* ps,
+                                                            int nbk, int64_t pcols, int8_t* pd) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= pcols * nbk) return;
+  const int64_t pc = t / nbk;
+  const int kb = (int)(t - pc * nbk);
+  const int64_t blkc = pc / 32;
+  const int n = (int)(pc - blkc * 32);
+  const int e = exp_from16(pe[pc * nbk + kb]);
+  const int sp = ps[2 * pc + 1];
+  const int s = e == kExpNaN ? 0 : e - ps[2 * pc];
+  const bool ok = sp <= kDigitSpread;
+  const int8_t* src = pk + ((blkc * nbk + kb) * 64) * 16;
+  int8_t* dst = pd + ((blkc * nbk + kb) * 128) * 16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+    if (ok) fold_digits16(*reinterpret_cast<const uint4*>(src + (n + 32 * h) * 16), s, d0, d1);
+    *reinterpret_cast<uint4*>(dst + (n + 32 * h) * 16) = d0;
+    *reinterpret_cast<uint4*>(dst + (64 + n + 32 * h) * 16) = d1;
+  }
 }
 
 // per group of gw real columns: smallest column exponent, largest column spread
@@ -218,7 +247,7 @@ bool linear_weight_verify_any_group(const void* wq, int out_f, int in_f, int flu
 
 LinearWeightHeader linear_weight_header(int out_f, int in_f, int gw, int flush, int bfloat) {
   LinearWeightHeader h{};
-  h.magic = kLinearWeightMagic; h.version = 2;
+  h.magic = kLinearWeightMagic; h.version = 3;
   h.out_f = out_f; h.in_f = in_f; h.gw = gw; h.flush = flush ? 1 : 0; h.bfloat = bfloat;
   return h;
 }
@@ -255,7 +284,11 @@ extern "C" int mxa_linear_weight_prep(const float* w, int32_t out_features, int3
                      reinterpret_cast<int8_t*>(wb + W.pk), reinterpret_cast<int16_t*>(wb + W.pe));
   if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   hipLaunchKernelGGL(linear_stats_kernel, dim3((unsigned)((pcols + 255) / 256)), dim3(256), 0, stream,
-                     reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps));
+                     reinterpret_cast<const int16_t*>(wb + W.pe), pcols, W.nbk, reinterpret_cast<int16_t*>(wb + W.ps),
+                     reinterpret_cast<int16_t*>(wb + W.pn));
+  hipLaunchKernelGGL(linear_digits_kernel, dim3((unsigned)((pcols * W.nbk + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const int8_t*>(wb + W.pk), reinterpret_cast<const int16_t*>(wb + W.pe),
+                     reinterpret_cast<const int16_t*>(wb + W.ps), W.nbk, pcols, reinterpret_cast<int8_t*>(wb + W.pd));
   hipLaunchKernelGGL(linear_group_stats_kernel, dim3((unsigned)((W.G + 63) / 64)), dim3(64), 0, stream,
                      reinterpret_cast<const int16_t*>(wb + W.ps), W.G, W.NB32, group_width,
                      reinterpret_cast<int16_t*>(wb + W.gs));

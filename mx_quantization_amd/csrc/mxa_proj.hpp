@@ -26,13 +26,35 @@
 
 namespace mxa {
 
-
+// 16 codes times 2^s (0 <= s <= kDigitSpread) as two signed base-256 digits:
+// c * 2^s = d0 + 256 d1, d0 in [-128, 127], |d1| <= 127
+__device__ __forceinline__ void fold_digits16(const uint4& v, int s, uint4& d0, uint4& d1) {
+  const uint32_t in[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o0[4], o1[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int c = (int)(int8_t)(in[w] >> (8 * b));
+      const int f = c << s;
+      const int lo = (int)(int8_t)f;
+      p0 |= ((uint32_t)lo & 0xFFu) << (8 * b);
+      p1 |= ((uint32_t)((f - lo) >> 8) & 0xFFu) << (8 * b);
+    }
+    o0[w] = p0;
+    o1[w] = p1;
+  }
+  d0 = make_uint4(o0[0], o0[1], o0[2], o0[3]);
+  d1 = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+}
 
 struct ProjLds {
-  size_t xt, xe, rlo, rhi, rn, st, ot, total;
+  size_t xt, xh, xe, rlo, rhi, rn, st, ot, total;
   int xst, ost;
 };
-// x code tile [32][Cpad + 16], x exponents relative to the row's smallest [nbk][32]
+// x code tile [32][Cpad + 16] (or its exponent-folded low digits; the high digits in a
+// second tile), x exponents relative to the row's smallest [nbk][32]
 // (int16, NaN -> 0), per-row smallest / largest exponent and NaN flag, tile stats, the
 // fp32 output tile of one head [32][96 NBD + 1]: q, k, v at columns 0, 32 NBD, 64 NBD
 // (padding columns beyond D take the padded MFMA columns, so every lane stores
@@ -45,6 +67,8 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   L.xst = Cpad + 16;
   L.xt = o;
   o += (size_t)32 * L.xst;
+  L.xh = o;
+  o += (size_t)32 * L.xst;
   L.xe = o;
   o += al((size_t)nbk * 32 * 2);
   L.rlo = o;
@@ -54,7 +78,7 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
   L.rn = o;
   o += 32 * 4;
   L.st = o;
-  o += 16;
+  o += 16;  // max row spread, smallest row exponent, the digit-path flag
   L.ost = 96 * ((D + 31) / 32) + 1;
   L.ot = o;
   o += al((size_t)32 * L.ost * 4);
@@ -64,6 +88,13 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 
 // One workgroup per (32-token block, image, head group), looping over the group's heads; 3 * NBD waves,
 // wave (s, cb) = sub-matrix s (q, k, v) and its 32-column block cb of the head.
+#ifndef MXA_PROJ_SKIP
+#define MXA_PROJ_SKIP 0  // tools-only timing variants (never the product): 1 no K loop, 2 no operand epilogue,
+                         // 4 the digit loop re-reads its first block (L1-resident weights)
+#endif
+#ifndef MXA_PROJ_APF
+#define MXA_PROJ_APF 0  // the digit loop's LDS operands loaded one block ahead (tools builds vary it)
+#endif
 #ifndef MXA_PROJ_WAVES
 #define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
 #endif
@@ -91,14 +122,7 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
   const int n0 = 32 * tb, rows = min(32, a.N - n0);
   const int64_t row0 = (int64_t)b * a.N + n0;
 
-  // ---- stage the token block's x codes (zero beyond N) and exponents ----------
-  const int cpr = a.Cpad / 16;
-  for (int i = threadIdx.x; i < 32 * cpr; i += kThreads) {
-    const int m = i / cpr, c = i - m * cpr;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (m < rows) v = *reinterpret_cast<const uint4*>(a.xc + (row0 + m) * a.Cpad + 16 * c);
-    *reinterpret_cast<uint4*>(xt + m * L.xst + 16 * c) = v;
-  }
+  // ---- the token block's x exponents, then its codes (zero beyond N) ----------------
   if (threadIdx.x < 32) {
     rlo[threadIdx.x] = 1 << 20;
     rhi[threadIdx.x] = -(1 << 20);
@@ -129,9 +153,35 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     const uint32_t smx = wave_reduce(lane < 32 ? (uint32_t)sp : 0u, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
     const uint32_t bmn = wave_reduce(lane < 32 ? (uint32_t)(lo + (1 << 20)) : 0xFFFFFFFFu,
                                      [](uint32_t u, uint32_t w) { return u < w ? u : w; });
+    // the digit path: every row's spread and every column spread of the workgroup's
+    // heads within kDigitSpread (the weight's folded digits exist for those columns)
+    uint32_t gmx = 0;
+    for (int i = lane; i < 3 * (h_end - h_begin); i += 64) {
+      const int hh = h_begin + i / 3, s3 = i - 3 * (i / 3);
+      gmx = max(gmx, (uint32_t)a.gs[2 * (s3 * a.H + hh) + 1]);
+    }
+    gmx = wave_reduce(gmx, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
     if (lane == 0) {
       st[0] = (int)smx;
       st[1] = (int)bmn - (1 << 20);
+      st[2] = !SLOW && smx <= kDigitSpread && gmx <= kDigitSpread;
+    }
+  }
+  __syncthreads();
+  const bool dig = !SLOW && st[2];  // uniform over the workgroup
+  int8_t* xh = reinterpret_cast<int8_t*>(smem + L.xh);
+  const int cpr = a.Cpad / 16;
+  for (int i = threadIdx.x; i < 32 * cpr; i += kThreads) {
+    const int m = i / cpr, c = i - m * cpr;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < rows) v = *reinterpret_cast<const uint4*>(a.xc + (row0 + m) * a.Cpad + 16 * c);
+    if (dig) {
+      uint4 d0, d1;
+      fold_digits16(v, xe[(c >> 1) * 32 + m], d0, d1);
+      *reinterpret_cast<uint4*>(xt + m * L.xst + 16 * c) = d0;
+      *reinterpret_cast<uint4*>(xh + m * L.xst + 16 * c) = d1;
+    } else {
+      *reinterpret_cast<uint4*>(xt + m * L.xst + 16 * c) = v;
     }
   }
   __syncthreads();
@@ -168,7 +218,8 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     // the result could be subnormal) the blocks are summed in fp64 by the slow kernel:
     // exact while their scaled exponents span <= 34 bits, within fp32 rounding beyond.
     // The decision is per head (the largest column spread of its q, k, v weight groups,
-    // uniform over the workgroup).
+    // uniform over the workgroup).  A workgroup whose row spreads and heads' column spreads
+    // are all <= kDigitSpread takes the exponent-folded operands instead (run_dig below).
     if constexpr (!SLOW) {
       int gsp = 0, glo = 1 << 20;
 #pragma unroll
@@ -177,13 +228,39 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         glo = min(glo, (int)a.gs[2 * g]);
         gsp = max(gsp, (int)a.gs[2 * g + 1]);
       }
-      if (!(st[0] + gsp <= a.smax && st[1] + glo >= -126)) {
+      // (the digit path's sums are exact at any spread it takes: only the subnormal test)
+      if (!((dig || st[0] + gsp <= a.smax) && st[1] + glo >= -126)) {
         if (threadIdx.x == 0) a.slow_list[atomicAdd(a.slow_count, 1)] = (b * a.ntb + tb) * a.H + h;
         continue;  // uniform over the workgroup
       }
     }
     const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
     const float bb = (a.bias && colv) ? (PLAIN ? a.bias[jcol] : round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1)) : 0.0f;
+    // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -------
+    // value(i, row_lo): element i's fp32 sum; branch-free: NaN by select; bb = 0 without
+    // a bias and o + 0 = o here (o is never -0: an integer sum converts to +0)
+    auto store_tile = [&](auto&& value, bool cn) {
+      float* orow = ot + m0 * kOst + s * 32 * NBD + dcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 lo4 = *reinterpret_cast<const int4*>(rlo + 8 * q + m0);
+        const int4 rn4 = *reinterpret_cast<const int4*>(rn + 8 * q + m0);
+        const int lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w}, nf[4] = {rn4.x, rn4.y, rn4.z, rn4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o = value(4 * q + r, lo[r]);
+          o = (cn || nf[r]) ? __uint_as_float(0x7FC00000u) : o;
+          if constexpr (PLAIN) {
+            o += bb;
+          } else {
+            o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
+            o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
+            if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
+          }
+          orow[(8 * q + r) * kOst] = o;
+        }
+      }
+    };
     // the K loop and the epilogue, specialised on the accumulation (FAST: shifted int32;
     // else fp64): separate live ranges, so the two never hold registers together
     auto run = [&](auto fast_c) {
@@ -283,33 +360,73 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         epi(cA, E2, xA);
       }
       if (r > 3) epi(cB, E3, xB);
-      // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) -------
-      // branch-free: NaN by select; bb = 0 without a bias and o + 0 = o here (o is never
-      // -0: an int32 sum converts to +0)
-      float* orow = ot + m0 * kOst + s * 32 * NBD + dcol;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int4 lo4 = *reinterpret_cast<const int4*>(rlo + 8 * q + m0);
-        const int4 rn4 = *reinterpret_cast<const int4*>(rn + 8 * q + m0);
-        const int lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w}, nf[4] = {rn4.x, rn4.y, rn4.z, rn4.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float o;
-          if constexpr (FAST) o = ldexpf((float)acc[4 * q + r], lo[r] + wlo);
-          else o = (float)acc[4 * q + r];
-          o = (cnan || nf[r]) ? __uint_as_float(0x7FC00000u) : o;
-          if constexpr (PLAIN) {
-            o += bb;
-          } else {
-            o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
-            o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
-            if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
-          }
-          orow[(8 * q + r) * kOst] = o;
-        }
-      }
+      store_tile(
+          [&](int i, int lo) {
+            if constexpr (FAST) return ldexpf((float)acc[i], lo + wlo);
+            else return (float)acc[i];
+          },
+          cnan);
     };
-    run(std::integral_constant<bool, !SLOW>{});
+    // Exponent-folded operands (dig): the tile's codes times 2^(block exponent - row's
+    // smallest) and the weight's times 2^(block exponent - column's smallest), each as two
+    // signed base-256 digits, so every block's scale is already in the operands: the four
+    // digit products accumulate in the MFMA's own int32 accumulators over all K-blocks
+    // (lo x lo; lo x hi + hi x lo; hi x hi: |sum| <= 2 nbk 32 128^2 < 2^31) with no VALU
+    // per block, and sum = c0 + 2^8 c1 + 2^16 c2 (exact in fp64) rounds once.
+    auto run_dig = [&]() {
+      const auto drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.pd), 0, a.pd_bytes, 0x00020000);
+      const int dsoff = __builtin_amdgcn_readfirstlane((int)(blkc * nbk) * 2048);
+      auto ldd = [&](int kb, int p) {
+        return __builtin_bit_cast(v4i_, __builtin_amdgcn_raw_buffer_load_b128(drs, woff, dsoff + ((MXA_PROJ_SKIP & 4) ? 0 : kb * 2048) + p * 1024, 0));
+      };
+      const int8_t* xha = xh + ln * L.xst + kh;
+      const int last = nbk - 1;
+      auto cl = [&](int kb) { return min(kb, last); };
+      v16i c0 = {}, c1 = {}, c2 = {};
+      // weight digits four blocks ahead (slot = block mod 4), the tile's from LDS
+      v4i_ L0 = ldd(0, 0), H0 = ldd(0, 1), L1 = ldd(cl(1), 0), H1 = ldd(cl(1), 1);
+      v4i_ L2 = ldd(cl(2), 0), H2 = ldd(cl(2), 1), L3 = ldd(cl(3), 0), H3 = ldd(cl(3), 1);
+#if MXA_PROJ_APF
+      v4i_ nal = *reinterpret_cast<const v4i_*>(xa), nah = *reinterpret_cast<const v4i_*>(xha);
+#endif
+      auto step = [&](int kb, v4i_& Ls, v4i_& Hs) {
+#if MXA_PROJ_APF
+        const v4i_ al = nal, ah = nah;  // the tile's digits one block ahead
+        nal = *reinterpret_cast<const v4i_*>(xa + 32 * cl(kb + 1));
+        nah = *reinterpret_cast<const v4i_*>(xha + 32 * cl(kb + 1));
+#else
+        const v4i_ al = *reinterpret_cast<const v4i_*>(xa + 32 * kb);
+        const v4i_ ah = *reinterpret_cast<const v4i_*>(xha + 32 * kb);
+#endif
+        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Ls, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Hs, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Hs, c2, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c1, 0, 0, 0);
+        Ls = ldd(cl(kb + 4), 0);
+        Hs = ldd(cl(kb + 4), 1);
+        __builtin_amdgcn_sched_barrier(0);  // reload each slot right after its use
+      };
+      int kb = 0;
+      for (; kb + 4 <= nbk; kb += 4) {
+        step(kb, L0, H0);
+        step(kb + 1, L1, H1);
+        step(kb + 2, L2, H2);
+        step(kb + 3, L3, H3);
+      }
+      if (kb < nbk) step(kb, L0, H0);
+      if (kb + 1 < nbk) step(kb + 1, L1, H1);
+      if (kb + 2 < nbk) step(kb + 2, L2, H2);
+      store_tile(
+          [&](int i, int lo) {
+            const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
+            return (float)ldexp(v, lo + wlo);
+          },
+          a.pn[pc] != 0);
+    };
+    if (MXA_PROJ_SKIP & 1) store_tile([](int, int) { return 0.0f; }, false);
+    else if (dig) run_dig();
+    else run(std::integral_constant<bool, !SLOW>{});
+
     __syncthreads();
     if (a.qkv_out) {  // the fp32 projection (tests): whole rows of the tile, coalesced
       for (int i = threadIdx.x; i < 32 * 3 * D; i += kThreads) {
@@ -326,7 +443,8 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     const int64_t hrow0 = (hrow_b + h) * a.N + n0;  // row of (b, h, n0) in the q / k tables
     constexpr int kPer = 32 * NBD * 2;              // lanes per sub-matrix: a multiple of 64
     static_assert(kThreads - 2 * kPer == 64 * NBD, "V lanes");
-    if ((int)threadIdx.x < 2 * kPer) {
+    if (MXA_PROJ_SKIP & 2) {
+    } else if ((int)threadIdx.x < 2 * kPer) {
       // rows_prep's per-block body on the tile (2 lanes per 32-element block)
       const int t = (int)threadIdx.x;
       const int sk = __builtin_amdgcn_readfirstlane(t / kPer);  // uniform per wave: q or k

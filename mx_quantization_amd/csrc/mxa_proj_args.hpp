@@ -6,19 +6,25 @@ namespace mxa {
 
 // Prepared Linear weight (mxa_linear_weight_prep): output columns in groups of gw (a
 // head's q, k or v: gw = D), each group padded to NB32 = ceil(gw/32) 32-column blocks.
+//   hdr the geometry and settings it was prepared with (LinearWeightHeader, 256 B at
+//       offset 0, so a buffer of any size holds it): mxa_qkv_attention refuses a buffer
+//       whose header does not match the call instead of reading past its end
+//   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from;
+//       first, so their offsets do not depend on gw: mxa_linear reads them for any gw)
 //   pk  MFMA-ready codes [group][cb][kb][lane 0..63][16 B]: lane = n + 32 h holds
 //       W[col n][32 kb + 16 h .. + 16] -- one coalesced 1-KB load per wave and K-block
 //   pe  block exponents [padded column][nbk] (int16, NaN = -32768)
 //   ps  per padded column: smallest finite block exponent, spread (int16 pair)
 //   gs  per group (of gw real columns): the smallest ps exponent, the largest spread
-//   raw row-major codes [out][Cpad] + exponents [out][nbk] (rows_prep output, packed from)
-//   hdr the geometry and settings it was prepared with (LinearWeightHeader, 256 B at
-//       offset 0, so a buffer of any size holds it): mxa_qkv_attention refuses a buffer
-//       whose header does not match the call instead of reading past its end
+//   pn  per padded column: 1 when a block exponent is NaN (int16)
+//   pd  exponent-folded codes [group][cb][kb][digit 0, 1][lane][16 B]: the code times
+//       2^(block exponent - column's smallest) as two signed base-256 digits (column
+//       spread <= kDigitSpread; else zeros, and the column's group never takes them)
 struct LinearLayout {
   int G, NB32, nbk, Cpad;
-  int64_t hdr, pk, pe, ps, gs, rawc, rawe, total;
+  int64_t hdr, rawc, rawe, pk, pe, ps, gs, pn, pd, total;
 };
+constexpr int kDigitSpread = 8;  // 127 * 2^8 < 2^15: two signed int8 digits
 constexpr uint32_t kLinearWeightMagic = 0x5741584du;  // "MXAW"
 struct LinearWeightHeader {
   uint32_t magic;
@@ -39,6 +45,10 @@ __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int g
   int64_t o = 0;
   L.hdr = o;
   o += 256;
+  L.rawc = o;
+  o += al((int64_t)out_f * L.Cpad);
+  L.rawe = o;
+  o += al((int64_t)out_f * L.nbk * 2);
   L.pk = o;
   o += al(pcols * L.Cpad);
   L.pe = o;
@@ -47,10 +57,10 @@ __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int g
   o += al(pcols * 4);
   L.gs = o;
   o += al((int64_t)L.G * 4);
-  L.rawc = o;
-  o += al((int64_t)out_f * L.Cpad);
-  L.rawe = o;
-  o += al((int64_t)out_f * L.nbk * 2);
+  L.pn = o;
+  o += al(pcols * 2);
+  L.pd = o;
+  o += al(2 * pcols * L.Cpad);
   L.total = o;
   return L;
 }
@@ -62,12 +72,14 @@ struct ProjArgs {
   const int16_t* pe;
   const int16_t* ps;
   const int16_t* gs;  // per weight group: smallest exponent, largest spread (the head's fast-path test)
+  const int16_t* pn;  // per padded column: NaN block flag
+  const int8_t* pd;   // exponent-folded digit codes
   int* slow_count;    // heads listed for qkv_proj_slow_kernel (zeroed before the launch)
   int* slow_list;     // (b * ntb + tb) * H + h
   const float* bias;  // [3*H*D] or null
   float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
   int B, N, H, D, nbk, Cpad, bfloat, ntb;
-  int pk_bytes, pe_bytes;  // buffer-descriptor extents of pk / pe (< 2 GiB: launch_proj checks)
+  int pk_bytes, pe_bytes, pd_bytes;  // buffer-descriptor extents of pk / pe / pd (< 2 GiB: launch_proj checks)
   int smax;  // largest exponent spread whose shifted int32 block sums cannot overflow
   int hpg;   // heads per workgroup (grid z = head groups: fills the last round of workgroups)
   int autocast;  // 0, or the dtype torch.autocast rounds the product to before the fp32 bias add

@@ -602,6 +602,38 @@ def test_qkv_attention_vs_oracle_chain(M, mode, B, N, C, H, k_top):
     same(host(out), host(o2), "out vs unfused op")
 
 
+@pytest.mark.parametrize("H", [4, 2])
+def test_qkv_projection_spread_paths(M, H):
+    """The fused projection's three accumulations in one launch, bit-exact against the
+    oracle: exponent-folded digits (row and column spreads <= 8), shifted int32 sums (row
+    spreads 9 .. smax, or a head whose weight columns spread 10), fp64 block sums (wider,
+    up to the 34-bit span they hold exactly).
+    Rows scale alternate 32-channel blocks by 2^s; one head's q columns by 2^10, another's
+    k columns by 2^8 (the digit limit itself); H = 2 (D = 128) the widest head."""
+    B, N, C = 2, 70, 256
+    D = C // H
+    rng = np.random.default_rng(11 + H)
+    x = rng.standard_normal((B, N, C), dtype=np.float32)
+    W = (rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(0.05)).astype(np.float32)
+    bias = (rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+    odd = (np.arange(C) // 32) % 2 == 1
+    shifts = [0, 3, 8, 9, 12, 20, 30]  # fp64 block sums are exact to a 34-bit span
+    for t in range(N):
+        s = shifts[(t // 5) % len(shifts)]  # whole token blocks mostly share one spread
+        x[:, t, odd] *= np.float32(2.0 ** s)
+    W[0 * C + 0 * D: 0 * C + 0 * D + D][:, odd] *= np.float32(2.0 ** 10)  # head 0's q columns
+    hk = min(1, H - 1)
+    W[1 * C + hk * D: 1 * C + hk * D + D][:, odd] *= np.float32(2.0 ** 8)  # a head's k columns
+    wq = M.LinearWeightMX(dev(W), D)
+    out, idx, qkv = M.mx_qkv_attention(dev(x), wq, dev(bias), H, D ** -0.5, k_top=10, return_qkv=True)
+    torch.cuda.synchronize()
+    same(host(qkv), O.mx_linear(x, W, bias), "qkv across the accumulation paths")
+    q, kk, v = (dev(np.ascontiguousarray(t)) for t in O.qkv_split(host(qkv), H))
+    o2, i2 = M.mx_topk_attention(q, kk, v, D ** -0.5, k_top=10)
+    same(host(idx), host(i2), "idx vs unfused op")
+    same(host(out), host(o2), "out vs unfused op")
+
+
 def test_qkv_weight_header_checked(M):
     """mxa_qkv_attention refuses a prepared weight whose header does not match the call
     (ADVICE r2): other settings, an unprepared buffer; a copy of a good one is accepted
