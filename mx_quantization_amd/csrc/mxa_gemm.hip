@@ -14,10 +14,11 @@ int gemm_smax(int nbk) {
   return s;
 }
 
-int64_t gemm_slow_bytes(int M, int Nc, int64_t batch) {
-  const int64_t tiles = (int64_t)((M + kGemmRows - 1) / kGemmRows) * ((Nc + kGemmCols - 1) / kGemmCols) * batch;
-  return (4 * (1 + 4 * tiles) + 255) / 256 * 256;
+// the fp64 kernel's list (count, then tile * 4 + wave entries), then the digit kernel's flag
+static int64_t gemm_tiles(int M, int Nc, int64_t batch) {
+  return (int64_t)((M + kGemmRows - 1) / kGemmRows) * ((Nc + kGemmCols - 1) / kGemmCols) * batch;
 }
+int64_t gemm_slow_bytes(int M, int Nc, int64_t batch) { return (4 * (2 + 4 * gemm_tiles(M, Nc, batch)) + 255) / 256 * 256; }
 
 // slow: gemm_slow_bytes of device scratch (the fp64 kernel's list)
 template <bool PLAIN>
@@ -31,6 +32,18 @@ static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, int* slow, hipStrea
                         reinterpret_cast<const void*>(&mx_gemm_slow_kernel<PLAIN>)})
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
   ga.slow = slow;
+  ga.dig_flag = nullptr;
+  if (ga.bpd && batch == 1 && ga.nbk <= kGemmDigNbkMax) {
+    // the exponent-folded digits first; the kernels below then run only if a row block
+    // could not take them
+    const size_t dl = gemm_dig_lds(ga.nbk).total;
+    const void* dk = reinterpret_cast<const void*>(&mx_gemm_dig_kernel<PLAIN>);
+    if (hipFuncSetAttribute(dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl) != hipSuccess) return MXA_ERR_LAUNCH;
+    ga.dig_flag = slow + 1 + 4 * gemm_tiles(ga.M, ga.Nc, 1);
+    if (hipMemsetAsync(ga.dig_flag, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
+    hipLaunchKernelGGL(mx_gemm_dig_kernel<PLAIN>, dim3((unsigned)((ga.M + 31) / 32)), dim3(256), dl, stream, ga);
+    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  }
   // grid.z <= 65535: larger batches in slices (each slice lists its slow waves by its own
   // batch index, so every slice runs its own fp64 pass)
   const int64_t esz = (ga.linear || ga.dt == kF32) ? 4 : 2;
@@ -74,6 +87,11 @@ int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int i
     const LinearLayout P = linear_layout(out_f, in_f, h.gw);
     g.bpk = reinterpret_cast<const int8_t*>(wb + P.pk);
     g.b_nb32 = P.G * P.NB32;
+    g.bpd = reinterpret_cast<const int8_t*>(wb + P.pd);
+    g.bps = reinterpret_cast<const int16_t*>(wb + P.ps);
+    g.bpn = reinterpret_cast<const int16_t*>(wb + P.pn);
+    g.bgs = reinterpret_cast<const int16_t*>(wb + P.gs);
+    g.bG = P.G;
   }
   g.linear = 1; g.dt = kF32; g.bfloat = bfloat; g.autocast = autocast; g.bias = bias;
   g.c = out; g.ldc = out_row_stride;

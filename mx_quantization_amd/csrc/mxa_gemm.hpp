@@ -79,6 +79,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   int* cn = reinterpret_cast<int*>(smem + L.cn);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m0g = tm * kGemmRows, n0g = tn * kGemmCols;
+  if constexpr (!SLOW) {  // every row block already taken by the digit kernel
+    if (a.dig_flag && __builtin_amdgcn_readfirstlane(*a.dig_flag) == 0) return;
+  }
   const int16_t* aeb = a.ae + bat * a.ae_bat;
   const int16_t* beb = a.be + bat * a.be_bat;
 
@@ -357,6 +360,175 @@ __global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
     const int tn = (int)(t % ntn), tm = (int)((t / ntn) % ntm);
     gemm_tile<true, PLAIN>(a, t / (ntn * ntm), tm, tn, w, smem);
     __syncthreads();  // the next entry restages the exponent tables
+  }
+}
+
+// ---- exponent-folded digits (mx.Linear with a prepared weight) ----------------------
+// One workgroup per 32-row block of A: the rows' codes times 2^(block exponent - row's
+// smallest) are staged in LDS as two signed base-256 digits (MFMA-ready: [kb][digit][lane]
+// [16 B]), the weight's digits (mxa_linear_weight_prep's pd) stream from memory, and the
+// four digit products accumulate in the MFMA's own int32 accumulators over all K-blocks
+// (lo x lo; lo x hi + hi x lo; hi x hi: |sum| <= 2 nbk 32 128^2 < 2^31) -- no VALU per
+// block -- so sum = c0 + 2^8 c1 + 2^16 c2 (exact in fp64) rounds once: the same correctly
+// rounded exact product as gemm_tile's shifted int32 sums.  A block whose row spreads or
+// the weight's column spreads exceed kDigitSpread (or whose result could be subnormal)
+// sets a.dig_flag, and the shifted-int32 kernels then run the whole product.
+struct GemmDigLds {
+  size_t ad, rlo, rhi, rn, st, total;
+};
+__host__ __device__ inline GemmDigLds gemm_dig_lds(int nbk) {
+  GemmDigLds L;
+  L.ad = 0;
+  L.rlo = (size_t)nbk * 2048;
+  L.rhi = L.rlo + 128;
+  L.rn = L.rhi + 128;
+  L.st = L.rn + 128;
+  L.total = L.st + 16;
+  return L;
+}
+constexpr int kGemmDigNbkMax = 72;  // 2 KB of LDS per K-block: <= 144 KB
+
+template <bool PLAIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void mx_gemm_dig_kernel(GemmArgs a) {
+  typedef int v16i_g __attribute__((ext_vector_type(16)));
+  typedef int v4i_g __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nbk = a.nbk;
+  const GemmDigLds L = gemm_dig_lds(nbk);
+  int8_t* ad = reinterpret_cast<int8_t*>(smem + L.ad);
+  int* rlo = reinterpret_cast<int*>(smem + L.rlo);
+  int* rhi = reinterpret_cast<int*>(smem + L.rhi);
+  int* rn = reinterpret_cast<int*>(smem + L.rn);
+  int* st = reinterpret_cast<int*>(smem + L.st);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rb = blockIdx.x, m0g = 32 * rb, rows = min(32, a.M - m0g);
+  auto code_at = [&](int m, int kb, int h) -> const int8_t* {  // 16 codes of row m, block kb, half h
+    return a.a_mfma ? a.a + (((int64_t)rb * nbk + kb) * 64 + m + 32 * h) * 16
+                    : a.a + (int64_t)(m0g + m) * a.lda + 32 * kb + 16 * h;
+  };
+  auto exp_at = [&](int m, int kb) { return exp_from16(a.ae[(int64_t)(m0g + m) * nbk + kb]); };
+
+  // ---- per row: smallest / largest finite block exponent (all-zero blocks left out, as
+  // in gemm_tile), NaN flag -------------------------------------------------------------
+  if (tid < 32) {
+    rlo[tid] = 1 << 20;
+    rhi[tid] = -(1 << 20);
+    rn[tid] = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < 32 * nbk; i += 256) {
+    const int m = i / nbk, kb = i - m * nbk;
+    if (m >= rows) continue;
+    const int e = exp_at(m, kb);
+    if (e == kExpNaN) {
+      rn[m] = 1;
+      continue;
+    }
+    if (e <= -128) {
+      const uint4 u = *reinterpret_cast<const uint4*>(code_at(m, kb, 0));
+      const uint4 v = *reinterpret_cast<const uint4*>(code_at(m, kb, 1));
+      if (((u.x | u.y | u.z | u.w) | (v.x | v.y | v.z | v.w)) == 0u) continue;
+    }
+    atomicMin(&rlo[m], e);
+    atomicMax(&rhi[m], e);
+  }
+  __syncthreads();
+  if (wave == 0) {  // the block's gate: row spreads, the weight's column spreads, subnormal results
+    const int m = lane & 31;
+    const bool em = rlo[m] > rhi[m];
+    const uint32_t smx = wave_reduce(lane < 32 && !em ? (uint32_t)(rhi[m] - rlo[m]) : 0u,
+                                     [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+    const uint32_t lmn = wave_reduce(lane < 32 && !em ? (uint32_t)(rlo[m] + (1 << 20)) : 0xFFFFFFFFu,
+                                     [](uint32_t u, uint32_t w) { return u < w ? u : w; });
+    uint32_t gsp = 0, glo = 0xFFFFFFFFu;
+    for (int g = lane; g < a.bG; g += 64) {
+      gsp = max(gsp, (uint32_t)a.bgs[2 * g + 1]);
+      glo = min(glo, (uint32_t)(a.bgs[2 * g] + (1 << 20)));
+    }
+    gsp = wave_reduce(gsp, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+    glo = wave_reduce(glo, [](uint32_t u, uint32_t w) { return u < w ? u : w; });
+    const bool ok = smx <= (uint32_t)kDigitSpread && gsp <= (uint32_t)kDigitSpread &&
+                    (lmn == 0xFFFFFFFFu || (int)lmn + (int)glo - (2 << 20) >= -126);
+    if (lane == 0) {
+      st[0] = ok;
+      if (!ok) atomicOr(a.dig_flag, 1);
+    }
+  }
+  __syncthreads();
+  if (!st[0]) return;  // uniform over the workgroup
+
+  // ---- the rows' digits: chunk (kb, lane) = row lane % 32, half lane / 32 ----------------
+  for (int i = tid; i < 64 * nbk; i += 256) {
+    const int kb = i >> 6, ln = i & 63, m = ln & 31;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    int sh = 0;
+    if (m < rows) {
+      v = *reinterpret_cast<const uint4*>(code_at(m, kb, ln >> 5));
+      const int e = exp_at(m, kb), lo = rlo[m] > rhi[m] ? 0 : rlo[m];
+      sh = e == kExpNaN ? 0 : min(max(e - lo, 0), kDigitSpread);  // (a left-out zero block: any shift)
+    }
+    uint4 d0, d1;
+    fold_digits16(v, sh, d0, d1);
+    *reinterpret_cast<uint4*>(ad + kb * 2048 + ln * 16) = d0;
+    *reinterpret_cast<uint4*>(ad + kb * 2048 + 1024 + ln * 16) = d1;
+  }
+  __syncthreads();
+
+  // ---- per wave: 32-column blocks wave, wave + 4, ... --------------------------------
+  const int ncb = (a.Nc + 31) / 32, last = nbk - 1;
+  const int ln = lane & 31, m0 = 4 * (lane >> 5);
+  const int8_t* adl = ad + lane * 16;
+  auto cl = [&](int kb) { return min(kb, last); };
+  for (int cb = wave; cb < ncb; cb += 4) {
+    const int8_t* bp = a.bpd + (int64_t)cb * nbk * 2048 + lane * 16;
+    auto ldd = [&](int kb, int p) { return *reinterpret_cast<const v4i_g*>(bp + (int64_t)kb * 2048 + p * 1024); };
+    v16i_g c0 = {}, c1 = {}, c2 = {};
+    v4i_g L0 = ldd(0, 0), H0 = ldd(0, 1), L1 = ldd(cl(1), 0), H1 = ldd(cl(1), 1);
+    v4i_g L2 = ldd(cl(2), 0), H2 = ldd(cl(2), 1), L3 = ldd(cl(3), 0), H3 = ldd(cl(3), 1);
+    auto step = [&](int kb, v4i_g& Ls, v4i_g& Hs) {
+      const v4i_g al = *reinterpret_cast<const v4i_g*>(adl + kb * 2048);
+      const v4i_g ah = *reinterpret_cast<const v4i_g*>(adl + kb * 2048 + 1024);
+      c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Ls, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Hs, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Hs, c2, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c1, 0, 0, 0);
+      Ls = ldd(cl(kb + 4), 0);
+      Hs = ldd(cl(kb + 4), 1);
+      __builtin_amdgcn_sched_barrier(0);  // reload each slot right after its use
+    };
+    int kb = 0;
+    for (; kb + 4 <= nbk; kb += 4) {
+      step(kb, L0, H0);
+      step(kb + 1, L1, H1);
+      step(kb + 2, L2, H2);
+      step(kb + 3, L3, H3);
+    }
+    if (kb < nbk) step(kb, L0, H0);
+    if (kb + 1 < nbk) step(kb + 1, L1, H1);
+    if (kb + 2 < nbk) step(kb + 2, L2, H2);
+    // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) ---------------
+    const int n = 32 * cb + ln;
+    if (n < a.Nc) {
+      const int clo = a.bps[2 * n];
+      const bool cnan = a.bpn[n] != 0;
+      const float bb = a.bias ? (PLAIN ? a.bias[n] : round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = 8 * (i >> 2) + m0 + (i & 3);
+        if (m >= rows) continue;
+        const int lo = rlo[m] > rhi[m] ? 0 : rlo[m];
+        const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
+        float o = (cnan || rn[m]) ? __uint_as_float(0x7FC00000u) : (float)ldexp(v, lo + clo);
+        if constexpr (PLAIN) {
+          o = a.bias ? o + bb : o;
+        } else {
+          // autocast: F.linear returns the dtype, then the output rounding, then + fp32 bias
+          o = round_bfloat(round_dt(o, a.autocast), a.bfloat, kRoundNearest, 1, a.autocast);
+          if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
+        }
+        static_cast<float*>(a.c)[(int64_t)(m0g + m) * a.ldc + n] = o;
+      }
+    }
   }
 }
 

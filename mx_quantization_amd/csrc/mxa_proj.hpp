@@ -26,29 +26,6 @@
 
 namespace mxa {
 
-// 16 codes times 2^s (0 <= s <= kDigitSpread) as two signed base-256 digits:
-// c * 2^s = d0 + 256 d1, d0 in [-128, 127], |d1| <= 127
-__device__ __forceinline__ void fold_digits16(const uint4& v, int s, uint4& d0, uint4& d1) {
-  const uint32_t in[4] = {v.x, v.y, v.z, v.w};
-  uint32_t o0[4], o1[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    uint32_t p0 = 0, p1 = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int c = (int)(int8_t)(in[w] >> (8 * b));
-      const int f = c << s;
-      const int lo = (int)(int8_t)f;
-      p0 |= ((uint32_t)lo & 0xFFu) << (8 * b);
-      p1 |= ((uint32_t)((f - lo) >> 8) & 0xFFu) << (8 * b);
-    }
-    o0[w] = p0;
-    o1[w] = p1;
-  }
-  d0 = make_uint4(o0[0], o0[1], o0[2], o0[3]);
-  d1 = make_uint4(o1[0], o1[1], o1[2], o1[3]);
-}
-
 struct ProjLds {
   size_t xt, xh, xe, rlo, rhi, rn, st, ot, total;
   int xst, ost;
@@ -92,6 +69,9 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #define MXA_PROJ_SKIP 0  // tools-only timing variants (never the product): 1 no K loop, 2 no operand epilogue,
                          // 4 the digit loop re-reads its first block (L1-resident weights)
 #endif
+#ifndef MXA_PROJ_C4
+#define MXA_PROJ_C4 0  // the digit loop's cross products in two accumulators (tools builds vary it)
+#endif
 #ifndef MXA_PROJ_APF
 #define MXA_PROJ_APF 0  // the digit loop's LDS operands loaded one block ahead (tools builds vary it)
 #endif
@@ -123,28 +103,64 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
   const int64_t row0 = (int64_t)b * a.N + n0;
 
   // ---- the token block's x exponents, then its codes (zero beyond N) ----------------
+  // When the tile's exponents and codes are at most four items per thread (DeiT, DiT),
+  // both are loaded into registers up front, so the code loads overlap the exponent
+  // passes and each exponent is read once; else they are (re)read where used.
+  const int cpr = a.Cpad / 16;
+  constexpr int kPre = 4;
+  const bool pre = 32 * cpr <= kPre * kThreads && 32 * nbk <= kPre * kThreads;  // uniform
+  uint4 cpre[kPre];
+  int epre[kPre];
+  auto code_of = [&](int i) {
+    const int m = i / cpr, c = i - m * cpr;
+    return m < rows ? *reinterpret_cast<const uint4*>(a.xc + (row0 + m) * a.Cpad + 16 * c) : make_uint4(0, 0, 0, 0);
+  };
+  auto exp_of = [&](int i) {
+    const int m = i / nbk, kb = i - m * nbk;
+    return m < rows ? exp_from16(a.xs[(row0 + m) * nbk + kb]) : 0;
+  };
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int i = (int)threadIdx.x + u * kThreads;
+      cpre[u] = i < 32 * cpr ? code_of(i) : make_uint4(0, 0, 0, 0);
+      epre[u] = i < 32 * nbk ? exp_of(i) : 0;
+    }
+  }
   if (threadIdx.x < 32) {
     rlo[threadIdx.x] = 1 << 20;
     rhi[threadIdx.x] = -(1 << 20);
     rn[threadIdx.x] = 0;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) {  // per row: finite min / max, NaN flag
-    const int m = i / nbk, kb = i - m * nbk;
-    const int e = m < rows ? exp_from16(a.xs[(row0 + m) * nbk + kb]) : 0;
+  auto take_exp = [&](int i, int e) {  // per row: finite min / max, NaN flag
+    const int m = i / nbk;
     if (e == kExpNaN) {
       rn[m] = 1;  // a NaN block makes the whole output row NaN
     } else {
       atomicMin(&rlo[m], e);
       atomicMax(&rhi[m], e);
     }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) {
+  };
+  auto put_xe = [&](int i, int e) {
     const int m = i / nbk, kb = i - m * nbk;
-    const int e = m < rows ? exp_from16(a.xs[(row0 + m) * nbk + kb]) : 0;
     const int lo = rlo[m] > rhi[m] ? 0 : rlo[m];
     xe[kb * 32 + m] = (int16_t)(e == kExpNaN ? 0 : e - lo);
+  };
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u)
+      if ((int)threadIdx.x + u * kThreads < 32 * nbk) take_exp((int)threadIdx.x + u * kThreads, epre[u]);
+  } else {
+    for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) take_exp(i, exp_of(i));
+  }
+  __syncthreads();
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u)
+      if ((int)threadIdx.x + u * kThreads < 32 * nbk) put_xe((int)threadIdx.x + u * kThreads, epre[u]);
+  } else {
+    for (int i = threadIdx.x; i < 32 * nbk; i += kThreads) put_xe(i, exp_of(i));
   }
   if (wave == 0) {  // tile stats over the 32 rows (lanes 32..63 neutral)
     const int m = lane & 31;
@@ -170,11 +186,8 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
   __syncthreads();
   const bool dig = !SLOW && st[2];  // uniform over the workgroup
   int8_t* xh = reinterpret_cast<int8_t*>(smem + L.xh);
-  const int cpr = a.Cpad / 16;
-  for (int i = threadIdx.x; i < 32 * cpr; i += kThreads) {
+  auto put_code = [&](int i, const uint4& v) {
     const int m = i / cpr, c = i - m * cpr;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (m < rows) v = *reinterpret_cast<const uint4*>(a.xc + (row0 + m) * a.Cpad + 16 * c);
     if (dig) {
       uint4 d0, d1;
       fold_digits16(v, xe[(c >> 1) * 32 + m], d0, d1);
@@ -183,6 +196,13 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     } else {
       *reinterpret_cast<uint4*>(xt + m * L.xst + 16 * c) = v;
     }
+  };
+  if (pre) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u)
+      if ((int)threadIdx.x + u * kThreads < 32 * cpr) put_code((int)threadIdx.x + u * kThreads, cpre[u]);
+  } else {
+    for (int i = threadIdx.x; i < 32 * cpr; i += kThreads) put_code(i, code_of(i));
   }
   __syncthreads();
 
@@ -383,6 +403,9 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
       const int last = nbk - 1;
       auto cl = [&](int kb) { return min(kb, last); };
       v16i c0 = {}, c1 = {}, c2 = {};
+#if MXA_PROJ_C4
+      v16i c3 = {};  // hi x lo apart from lo x hi: no accumulator feeds the next MFMA but one
+#endif
       // weight digits four blocks ahead (slot = block mod 4), the tile's from LDS
       v4i_ L0 = ldd(0, 0), H0 = ldd(0, 1), L1 = ldd(cl(1), 0), H1 = ldd(cl(1), 1);
       v4i_ L2 = ldd(cl(2), 0), H2 = ldd(cl(2), 1), L3 = ldd(cl(3), 0), H3 = ldd(cl(3), 1);
@@ -401,7 +424,11 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Ls, c0, 0, 0, 0);
         c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Hs, c1, 0, 0, 0);
         c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Hs, c2, 0, 0, 0);
+#if MXA_PROJ_C4
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c3, 0, 0, 0);
+#else
         c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c1, 0, 0, 0);
+#endif
         Ls = ldd(cl(kb + 4), 0);
         Hs = ldd(cl(kb + 4), 1);
         __builtin_amdgcn_sched_barrier(0);  // reload each slot right after its use
@@ -418,7 +445,11 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
       if (kb + 2 < nbk) step(kb + 2, L2, H2);
       store_tile(
           [&](int i, int lo) {
+#if MXA_PROJ_C4
+            const double v = (double)c0[i] + 256.0 * ((double)c1[i] + (double)c3[i]) + 65536.0 * (double)c2[i];
+#else
             const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
+#endif
             return (float)ldexp(v, lo + wlo);
           },
           a.pn[pc] != 0);

@@ -65,6 +65,29 @@ __host__ __device__ inline LinearLayout linear_layout(int out_f, int in_f, int g
   return L;
 }
 
+// 16 codes times 2^s (0 <= s <= kDigitSpread) as two signed base-256 digits:
+// c * 2^s = d0 + 256 d1, d0 in [-128, 127], |d1| <= 127
+__device__ __forceinline__ void fold_digits16(const uint4& v, int s, uint4& d0, uint4& d1) {
+  const uint32_t in[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o0[4], o1[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int c = (int)(int8_t)(in[w] >> (8 * b));
+      const int f = c << s;
+      const int lo = (int)(int8_t)f;
+      p0 |= ((uint32_t)lo & 0xFFu) << (8 * b);
+      p1 |= ((uint32_t)((f - lo) >> 8) & 0xFFu) << (8 * b);
+    }
+    o0[w] = p0;
+    o1[w] = p1;
+  }
+  d0 = make_uint4(o0[0], o0[1], o0[2], o0[3]);
+  d1 = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+}
+
 struct ProjArgs {
   const int8_t* xc;   // x codes [B*N][Cpad]
   const int16_t* xs;  // x code-unit exponents [B*N][nbk]
@@ -107,6 +130,15 @@ struct GemmArgs {
   const int8_t* bpk;
   int b_nb32;  // 32-column blocks in bpk
   int a_mfma;  // A codes in rows_prep's MFMA-ready layout ([M / 32][nbk][lane][16 B] per batch; lda unused)
+  // the prepared weight's exponent-folded digits (mx_gemm_dig_kernel; mx.Linear only): pd,
+  // per padded column (= output column here) smallest exponent (ps) and NaN flag (pn), the
+  // group stats gs of its bG groups
+  const int8_t* bpd;
+  const int16_t *bps, *bpn, *bgs;
+  int bG;
+  // set (non-zero) by mx_gemm_dig_kernel when a row block could not take the digits: the
+  // shifted-int32 kernels then run the whole product; null = no digit kernel ran
+  int* dig_flag;
 };
 
 }  // namespace mxa

@@ -35,6 +35,10 @@
 
 namespace mxa {
 
+#ifndef MXA_GRP_ELEM_X
+#define MXA_GRP_ELEM_X 1  // 32-position windows exchange elements, not positions (tools builds vary it)
+#endif
+
 typedef __attribute__((address_space(3))) uint32_t lu32;
 typedef __attribute__((address_space(3))) uint16_t lu16;
 typedef __attribute__((address_space(3))) uint8_t lu8;
@@ -164,12 +168,13 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // the median's iter_swap is applied to the stop masks in registers and written back
   // while the masks are formed (position f is never a stop; position m holds old f)
   const uint64_t xf = g.A[fa], xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1];
-  uint32_t K[E];
+  uint32_t K[E], I2[2];
 #pragma unroll
   for (int e = 0; e < E; e += 2) {
     const u32x4 v = *(const lu128*)(g.A + lb + e);
     K[e] = v.y;
     K[e + 1] = v.w;
+    if (E == 2) I2[0] = v.x, I2[1] = v.z;  // whole elements: the exchange below moves them
   }
   const uint32_t ka = hi32(xa), kb = hi32(xb), kc = hi32(xc);
   // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free:
@@ -228,6 +233,33 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // row at a time (only the swaps move: ~range/4 of the positions)
   // (u8 slots: the slot values are LDS byte addresses, the base folded into the
   // popcount accumulations)
+  if constexpr (E == 2 && NP <= 256 && MXA_GRP_ELEM_X) {
+    // a 32-position window (nsw <= 15): the swapping stops publish their ELEMENTS (right
+    // stop of top rank t at slot t, left stop of rank t at slot 16 + t -- 256 B of P), and
+    // each reads its partner's straight into its own position: one round trip fewer than
+    // publishing positions.  Position m holds old f since the median swap.
+    lu64* xs = (lu64*)(lu32*)g.P;
+    uint64_t el[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) el[e] = lb + e == m ? xf : (((uint64_t)K[e] << 32) | I2[e]);
+    int tg[2], sw[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int sh = 1 - e;
+      const int tl = (int)(PL + (uint32_t)__popc((Lm >> sh) >> 1));
+      const int tr = (int)(totR - PR - (uint32_t)__popc(Rm >> sh));
+      const bool isl = (SLm >> sh) & 1u, isr = ((Rm >> sh) & 1u) && (uint32_t)tr < nsw;
+      sw[e] = isl ? 1 : (isr ? 2 : 0);
+      tg[e] = isl ? tl : tr;
+      if (sw[e]) xs[(sw[e] == 1 ? 16 : 0) + tg[e]] = el[e];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (sw[e]) g.A[lb + e] = xs[(sw[e] == 1 ? 0 : 16) + tg[e]];
+    wave_lds_sync();
+    return cut;
+  }
   const uint32_t ob = NP <= 256 ? (uint32_t)(size_t)g.P : 0u;
   const uint32_t trash = ob + 2 * HP + gl, lbase = ob + HP + PL, rbase = ob + totR - PR, rlim = ob + nsw;
 #pragma unroll
