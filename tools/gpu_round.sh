@@ -10,7 +10,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out
-T=${TAG:-r04v2}
+T=${TAG:-r04v3}
 mkdir -p $O
 if [ -z "${NOTEST:-}" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > $O/${T}_pytest_gpu.log 2>&1

@@ -33,7 +33,7 @@ def stage_of(kernel):
         return "prep"
     if "qkv_proj_kernel" in kernel:
         return "proj"
-    if "mx_gemm_kernel" in kernel:
+    if "mx_gemm_kernel" in kernel or "mx_gemm_dig_kernel" in kernel:
         return "proj_linear"
     return None
 
