@@ -69,6 +69,9 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #define MXA_PROJ_SKIP 0  // tools-only timing variants (never the product): 1 no K loop, 2 no operand epilogue,
                          // 4 the digit loop re-reads its first block (L1-resident weights)
 #endif
+#ifndef MXA_PROJ_PRIO
+#define MXA_PROJ_PRIO 0  // wave priority of the digit K loop (tools builds vary it)
+#endif
 #ifndef MXA_PROJ_C4
 #define MXA_PROJ_C4 0  // the digit loop's cross products in two accumulators (tools builds vary it)
 #endif
@@ -434,6 +437,9 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         __builtin_amdgcn_sched_barrier(0);  // reload each slot right after its use
       };
       int kb = 0;
+#if MXA_PROJ_PRIO
+      __builtin_amdgcn_s_setprio(MXA_PROJ_PRIO);  // MFMA-phase waves issue first (tools builds)
+#endif
       for (; kb + 4 <= nbk; kb += 4) {
         step(kb, L0, H0);
         step(kb + 1, L1, H1);
@@ -443,6 +449,9 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
       if (kb < nbk) step(kb, L0, H0);
       if (kb + 1 < nbk) step(kb + 1, L1, H1);
       if (kb + 2 < nbk) step(kb + 2, L2, H2);
+#if MXA_PROJ_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       store_tile(
           [&](int i, int lo) {
 #if MXA_PROJ_C4
