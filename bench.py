@@ -256,8 +256,10 @@ def _unique_kernel(d, stage):
 
 
 def stage_of_kernel(name):
-    if "select_kernel" in name or "select_wave_kernel" in name:
+    if "select_q_kernel" in name:  # the packed-element selection kernel
         return "select"
+    if "select_kernel" in name:  # the 64-bit one: rows the packed kernel leaves, true scores, ELSA
+        return "select_fb"
     if "finish_kernel" in name or "finish16_kernel" in name or "dense_rows_kernel" in name:
         return "finish"
     if "attn_prep_kernel" in name:
@@ -672,6 +674,10 @@ def main(argv=None, run=run_config):
         "stages_ms": stages,
         "e2e": e2e,
         "cpu_baseline": cpu,
+        # what torch.distributed saw (a SCALE record shows RCCL ran N ranks)
+        "dist": {"initialized": dist.is_initialized(),
+                 "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                 "backend": dist.get_backend() if dist.is_initialized() else None},
     }
 
     if not args.no_parity:  # a sample of every rank's shard, gathered to rank 0

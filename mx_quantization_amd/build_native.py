@@ -13,11 +13,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmxa.so")
-# (source, object suffix, defines): mxa_sel.hip is compiled three times, one part of the
-# selection kernel's instantiations each (MXA_SEL_PART), so that the parts build in parallel
-UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", "", ("MXA_SEL_PART=0",)),
-         ("mxa_sel.hip", "_p1", ("MXA_SEL_PART=1",)), ("mxa_sel.hip", "_p2", ("MXA_SEL_PART=2",)),
-         ("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
+# (source, object suffix, defines): mxa_sel.hip is compiled seven times, the dispatcher and
+# one score mode's selection kernels each (MXA_SEL_PART), so that the parts build in parallel
+UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", "", ("MXA_SEL_PART=0",))]
+UNITS += [("mxa_sel.hip", f"_p{i}", (f"MXA_SEL_PART={i}",)) for i in range(1, 7)]
+UNITS += [("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
            "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_finish16.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",

@@ -36,12 +36,8 @@ constexpr int kFin16 = 16;  // query rows per MFMA tile (one wave)
 #ifndef MXA_FIN16_OCC  // waves per SIMD the register allocation aims at
 #define MXA_FIN16_OCC 4
 #endif
-// 1: V^T codes staged in LDS with the K table; 0: the MFMA B operands straight from
-// memory (measured at DeiT-base: 0.200 ms with 4 waves per SIMD, against 0.214 ms staged
-// at 3 waves per SIMD -- the staged table and a prefetched input set cost the fourth wave)
-#ifndef MXA_FIN16_VTLDS
-#define MXA_FIN16_VTLDS 0
-#endif
+// (the MFMA B operands, V^T codes, come straight from memory: staged in LDS with the K
+// table they measured 0.214 ms at 3 waves per SIMD against 0.200 ms at 4, DeiT-base)
 
 typedef int v4i16_ __attribute__((ext_vector_type(4)));
 
@@ -59,7 +55,6 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   L.ke = o;
   o += al((size_t)T * nbd * 2);
   L.vt = o;
-  if (MXA_FIN16_VTLDS) o += al((size_t)ntb * D * 32);  // [ntb][D][32]: the HBM layout
   L.ve = o;
   o += al((size_t)ntb * D * 2);
   L.waves = o;
@@ -84,7 +79,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
   int16_t* tve = reinterpret_cast<int16_t*>(smem + L.ve);
-  int8_t* tvt = reinterpret_cast<int8_t*>(smem + L.vt);
   unsigned char* wb = smem + L.waves + (size_t)wave * L.per_wave;
   int8_t* ptile = reinterpret_cast<int8_t*>(wb);
   float* sP = reinterpret_cast<float*>(wb + L.sp);
@@ -105,10 +99,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tke[i] = a.ksT[kb * nbd + i];
     const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
     for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tve[i] = vssrc[i];
-    if (MXA_FIN16_VTLDS) {  // V^T codes as they lie in HBM ([ntb][D][32] per head: one contiguous copy)
-      const uint4* vsrc = reinterpret_cast<const uint4*>(a.vt + (int64_t)bh * D * a.tpad);
-      for (int i = threadIdx.x; i < ntb * D * 2; i += blockDim.x) reinterpret_cast<uint4*>(tvt)[i] = vsrc[i];
-    }
     for (int i = lane; i < kFin16 * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
     for (int i = lane; i < kFin16 * ntb; i += 64) bmw[i] = 0u;
   }
@@ -241,7 +231,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     // codes are [ntb][D][32], so the operand of (block b, columns dt..dt+15) is one
     // contiguous 512-B run.
     const int ln = lane & 15, kg = lane >> 4;
-    const int8_t* vbase = (MXA_FIN16_VTLDS ? tvt : a.vt + (int64_t)bh * D * a.tpad) + 8 * kg;
+    const int8_t* vbase = a.vt + (int64_t)bh * D * a.tpad + 8 * kg;
     for (int dt = 0; dt < D; dt += 16) {
       const int d = min(dt + ln, D - 1);
       float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};

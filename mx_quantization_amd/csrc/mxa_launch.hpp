@@ -10,8 +10,23 @@ inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr
 
 // selection kernel (mxa_sel.hip); plan: only check the LDS budget, launch nothing
 int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);
-int launch_select_p1(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);  // OpExp, OpMul
-int launch_select_p2(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);  // TrueEx, Elsa, True
+// one score mode per translation unit of mxa_sel.hip (MXA_SEL_PART 1..6)
+int launch_select_p1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // ex_pred
+int launch_select_p2(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // EXION
+int launch_select_p3(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // MXINT4 / partial
+int launch_select_p4(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // true_ex
+int launch_select_p5(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // ELSA
+int launch_select_p6(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // the true scores
+inline int launch_select_mode(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
+  switch (mode) {
+    case kModeExSign: return launch_select_p1(ra, BH, stream, plan);
+    case kModeOpMul: return launch_select_p2(ra, BH, stream, plan);
+    case kModeOpExp: return launch_select_p3(ra, BH, stream, plan);
+    case kModeTrueEx: return launch_select_p4(ra, BH, stream, plan);
+    case kModeElsa: return launch_select_p5(ra, BH, stream, plan);
+    default: return launch_select_p6(ra, BH, stream, plan);
+  }
+}
 // the row kernel of the path: finishing kernel (top-k) or dense row kernel (mxa_fin.hip)
 int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan);
 // fused qkv projection kernel (mxa_proj.hip)

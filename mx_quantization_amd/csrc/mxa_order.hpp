@@ -23,30 +23,43 @@ __device__ __forceinline__ uint32_t order_key(float f) {
 }
 
 __device__ __forceinline__ uint64_t pack_ki(uint32_t key, uint32_t idx) { return ((uint64_t)key << 32) | idx; }
+// the packed element of a row of <= 256 keys: (order key & 0xFFFFFF00) | index
+__device__ __forceinline__ uint32_t qelem(uint32_t key, uint32_t idx) { return (key & 0xFFFFFF00u) | idx; }
+// nonzero when a score's fp32 bits need the key's low byte (a nonzero low mantissa byte;
+// NaN keys are all ones and pack)
+__device__ __forceinline__ uint32_t q_bad_bits(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x7FFFFFFFu) > 0x7F800000u ? 0u : (u & 0xFFu);
+}
 
 __device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
 
 typedef __attribute__((address_space(3))) uint64_t lu64;
 typedef __attribute__((address_space(3))) int li32;
 
+// cmp on elements: (key << 32 | index), or the packed (key & ~0xFF) | index of
+// mxa_topk_grp.hpp (key(x) > key(y) <=> x > (y | 0xFF))
 __device__ __forceinline__ bool lgt(uint64_t x, uint64_t y) { return (uint32_t)(x >> 32) > (uint32_t)(y >> 32); }
+__device__ __forceinline__ bool lgt(uint32_t x, uint32_t y) { return x > (y | 0xFFu); }
 
-// ---- stl_heap.h on one lane's row ------------------------------------------
-__device__ __forceinline__ void ln_push_heap(lu64* f, int hole, int top, uint64_t v) {
+// ---- stl_heap.h on one lane's row (LP: an LDS element type) ---------------------
+template <typename LP, typename V>
+__device__ __forceinline__ void ln_push_heap(LP* f, int hole, int top, V v) {
   int parent = (hole - 1) / 2;
-  while (hole > top && lgt(f[parent], v)) {
+  while (hole > top && lgt((V)f[parent], v)) {
     f[hole] = f[parent];
     hole = parent;
     parent = (hole - 1) / 2;
   }
   f[hole] = v;
 }
-__device__ __forceinline__ void ln_adjust_heap(lu64* f, int hole, int len, uint64_t v) {
+template <typename LP, typename V>
+__device__ __forceinline__ void ln_adjust_heap(LP* f, int hole, int len, V v) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
     second = 2 * (second + 1);
-    if (lgt(f[second], f[second - 1])) second--;
+    if (lgt((V)f[second], (V)f[second - 1])) second--;
     f[hole] = f[second];
     hole = second;
   }
@@ -57,27 +70,30 @@ __device__ __forceinline__ void ln_adjust_heap(lu64* f, int hole, int len, uint6
   }
   ln_push_heap(f, hole, top, v);
 }
-__device__ __forceinline__ void ln_pop_heap(lu64* first, int len, lu64* result) {
-  const uint64_t v = *result;
+template <typename LP>
+__device__ __forceinline__ void ln_pop_heap(LP* first, int len, LP* result) {
+  const auto v = +*result;
   *result = *first;
   ln_adjust_heap(first, 0, len, v);
 }
 // __heap_select(first, middle, last) on a[first..last)
-__device__ inline void ln_heap_select(lu64* a, int first, int middle, int last) {
-  lu64* f = a + first;
+template <typename LP>
+__device__ inline void ln_heap_select(LP* a, int first, int middle, int last) {
+  LP* f = a + first;
   const int len = middle - first;
   if (len >= 2) {  // __make_heap
     int parent = (len - 2) / 2;
     while (true) {
-      ln_adjust_heap(f, parent, len, f[parent]);
+      ln_adjust_heap(f, parent, len, +f[parent]);
       if (parent == 0) break;
       parent--;
     }
   }
   for (int i = middle; i < last; ++i)
-    if (lgt(a[i], f[0])) ln_pop_heap(f, len, a + i);
+    if (lgt(+a[i], +f[0])) ln_pop_heap(f, len, a + i);
 }
-__device__ inline void ln_sort_heap(lu64* a, int first, int last) {
+template <typename LP>
+__device__ inline void ln_sort_heap(LP* a, int first, int last) {
   while (last - first > 1) {
     --last;
     ln_pop_heap(a + first, last - first, a + last);
@@ -87,16 +103,17 @@ __device__ inline void ln_sort_heap(lu64* a, int first, int last) {
 // ---- stl_algo.h --------------------------------------------------------------
 // __insertion_sort(first, last) (guarded form; the unguarded inner loop of
 // __final_insertion_sort stops at the same element)
-__device__ __forceinline__ void ln_insertion_sort(lu64* a, int f, int l) {
+template <typename LP>
+__device__ __forceinline__ void ln_insertion_sort(LP* a, int f, int l) {
   for (int i = f + 1; i < l; ++i) {
-    const uint64_t v = a[i];
+    const auto v = +a[i];
     int j = i;
-    uint64_t prev = a[j - 1];
+    auto prev = +a[j - 1];
     while (lgt(v, prev)) {
       a[j] = prev;
       --j;
       if (j == f) break;
-      prev = a[j - 1];
+      prev = +a[j - 1];
     }
     a[j] = v;
   }

@@ -154,9 +154,6 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
       best_g = g;
     }
   }
-#ifdef MXA_PROJ_NG  // tools builds: a fixed head-group count
-  best_g = std::min(pa.H, MXA_PROJ_NG);
-#endif
   p.hpg = (pa.H + best_g - 1) / best_g;
   const int ng = (pa.H + p.hpg - 1) / p.hpg;
   hipLaunchKernelGGL((qkv_proj_kernel<NBD, PLAIN>), dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),

@@ -69,18 +69,6 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 #define MXA_PROJ_SKIP 0  // tools-only timing variants (never the product): 1 no K loop, 2 no operand epilogue,
                          // 4 the digit loop re-reads its first block (L1-resident weights)
 #endif
-#ifndef MXA_PROJ_PRIO
-#define MXA_PROJ_PRIO 0  // wave priority of the digit K loop (tools builds vary it)
-#endif
-#ifndef MXA_PROJ_C4
-#define MXA_PROJ_C4 0  // the digit loop's cross products in two accumulators (tools builds vary it)
-#endif
-#ifndef MXA_PROJ_APF
-#define MXA_PROJ_APF 0  // the digit loop's LDS operands loaded one block ahead (tools builds vary it)
-#endif
-#ifndef MXA_PROJ_WAVES
-#define MXA_PROJ_WAVES 4  // waves per SIMD the register budget targets (tools builds vary it)
-#endif
 // PLAIN (proj_plain): no bfloat rounding, no flush, no autocast, q / k operands of
 // rows_prep_block_plain and V's MXINT8 -- the bench path, compiled without the general
 // rounding code (a third of the code and registers of the general instantiation).
@@ -276,8 +264,9 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
           if constexpr (PLAIN) {
             o += bb;
           } else {
-            o = round_bfloat(o, a.bfloat, kRoundNearest, 1);
-            o = round_dt(o, a.autocast);  // autocast: F.linear returns the dtype, + fp32 bias promotes back
+            // autocast: F.linear returns the autocast dtype, quantize_elemwise_op rounds that
+            // (as mx_gemm's epilogue); + fp32 bias promotes back
+            o = round_bfloat(round_dt(o, a.autocast), a.bfloat, kRoundNearest, 1, a.autocast);
             if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
           }
           orow[(8 * q + r) * kOst] = o;
@@ -406,40 +395,21 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
       const int last = nbk - 1;
       auto cl = [&](int kb) { return min(kb, last); };
       v16i c0 = {}, c1 = {}, c2 = {};
-#if MXA_PROJ_C4
-      v16i c3 = {};  // hi x lo apart from lo x hi: no accumulator feeds the next MFMA but one
-#endif
       // weight digits four blocks ahead (slot = block mod 4), the tile's from LDS
       v4i_ L0 = ldd(0, 0), H0 = ldd(0, 1), L1 = ldd(cl(1), 0), H1 = ldd(cl(1), 1);
       v4i_ L2 = ldd(cl(2), 0), H2 = ldd(cl(2), 1), L3 = ldd(cl(3), 0), H3 = ldd(cl(3), 1);
-#if MXA_PROJ_APF
-      v4i_ nal = *reinterpret_cast<const v4i_*>(xa), nah = *reinterpret_cast<const v4i_*>(xha);
-#endif
       auto step = [&](int kb, v4i_& Ls, v4i_& Hs) {
-#if MXA_PROJ_APF
-        const v4i_ al = nal, ah = nah;  // the tile's digits one block ahead
-        nal = *reinterpret_cast<const v4i_*>(xa + 32 * cl(kb + 1));
-        nah = *reinterpret_cast<const v4i_*>(xha + 32 * cl(kb + 1));
-#else
         const v4i_ al = *reinterpret_cast<const v4i_*>(xa + 32 * kb);
         const v4i_ ah = *reinterpret_cast<const v4i_*>(xha + 32 * kb);
-#endif
         c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Ls, c0, 0, 0, 0);
         c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, Hs, c1, 0, 0, 0);
         c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Hs, c2, 0, 0, 0);
-#if MXA_PROJ_C4
-        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c3, 0, 0, 0);
-#else
         c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, Ls, c1, 0, 0, 0);
-#endif
         Ls = ldd(cl(kb + 4), 0);
         Hs = ldd(cl(kb + 4), 1);
         __builtin_amdgcn_sched_barrier(0);  // reload each slot right after its use
       };
       int kb = 0;
-#if MXA_PROJ_PRIO
-      __builtin_amdgcn_s_setprio(MXA_PROJ_PRIO);  // MFMA-phase waves issue first (tools builds)
-#endif
       for (; kb + 4 <= nbk; kb += 4) {
         step(kb, L0, H0);
         step(kb + 1, L1, H1);
@@ -449,16 +419,9 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
       if (kb < nbk) step(kb, L0, H0);
       if (kb + 1 < nbk) step(kb + 1, L1, H1);
       if (kb + 2 < nbk) step(kb + 2, L2, H2);
-#if MXA_PROJ_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       store_tile(
           [&](int i, int lo) {
-#if MXA_PROJ_C4
-            const double v = (double)c0[i] + 256.0 * ((double)c1[i] + (double)c3[i]) + 65536.0 * (double)c2[i];
-#else
             const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
-#endif
             return (float)ldexp(v, lo + wlo);
           },
           a.pn[pc] != 0);
@@ -521,7 +484,7 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
 }
 
 template <int NBD, bool PLAIN>
-__global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(MXA_PROJ_WAVES, 8))) void qkv_proj_kernel(ProjArgs a) {
+__global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(4, 8))) void qkv_proj_kernel(ProjArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   proj_block<NBD, PLAIN, false>(a, blockIdx.x, blockIdx.y, (int)blockIdx.z * a.hpg,
                                 min(a.H, ((int)blockIdx.z + 1) * a.hpg), smem);

@@ -45,6 +45,7 @@ struct Rows2Args {
   int waves;        // waves per workgroup
   int rows_per_wg;  // query rows per workgroup (grid.y splits a head when there are few heads)
   int32_t* idx32;  // split path: the kept indices [B*H*N][k_top] between the two kernels
+  int fb_only;     // selection kernel: only the rows the packed-element kernel left (idx32[row][0] < 0)
   // finishing kernel with the proj Linear behind it (D % 32 == 0): the output rows
   // (B, N, H*D) MX-quantized along C straight from the P.V tile -- rows_prep's layout,
   // codes [B*N][H*D], code-unit exponents [B*N][H*D/32] -- instead of fp32 in `out`

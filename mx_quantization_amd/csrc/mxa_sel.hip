@@ -6,17 +6,17 @@
 namespace mxa {
 
 // ---- selection kernel (mxa_select.hpp): four query rows per wave -------------------
-template <int NP, int MODE, int W>
+template <int NP, int MODE, int W, typename El>
 static size_t select_lds(const Rows2Args& ra) {
-  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP);
+  return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP, sizeof(El));
 }
-template <int NP, int MODE, int W>
+template <int NP, int MODE, int W, typename El = uint64_t, int QM = 0>
 static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
   Rows2Args ra = ra0;
-  const size_t lds = select_lds<NP, MODE, W>(ra);
+  const size_t lds = select_lds<NP, MODE, W, El>(ra);
   if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   if (plan) return MXA_OK;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W, El, QM>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
@@ -24,32 +24,31 @@ static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, boo
   while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
   ra.rows_per_wg = rows;
   const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_kernel<NP, MODE, W>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-// ---- selection kernel, one wave per query row (mxa_select.hpp select_wave_kernel) ----
-template <int NP, int MODE>
-static int launch_select_wave(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
-  Rows2Args ra = ra0;
-  const size_t lds = selw_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd);
-  if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  if (plan) return MXA_OK;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_wave_kernel<NP, MODE>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
-  int rows = kSelRows;
-  while (rows > kSelWaveW && (int64_t)BH * ((ra.N + rows - 1) / rows) < 4096) rows -= kSelWaveW;
-  ra.rows_per_wg = rows;
-  const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_wave_kernel<NP, MODE>), dim3((unsigned)BH, gy), dim3(64 * kSelWaveW), lds, stream, ra);
+  hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if constexpr (MXA_SEL_WAVE) return launch_select_wave<NP, MODE>(ra, BH, stream, plan);
-  if (sel_waves_for(ra.T, BH, ra.N) == 2) return launch_select_w<NP, MODE, 2>(ra, BH, stream, plan);
-  return launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
+  const int wsel = sel_waves_for(ra.T, BH, ra.N);
+  // packed elements (rows of <= 256 keys) for the approximators whose scores are sums of
+  // small integers times powers of two; then the 64-bit kernel on the rows whose scores do
+  // not pack (fb_only: its workgroups without such rows return at once).  The true scores,
+  // ELSA and longer rows: the 64-bit kernel alone.
+  constexpr bool kPack = MODE == kModeExSign || MODE == kModeOpExp || MODE == kModeOpMul || MODE == kModeTrueEx;
+  if constexpr (kPack && NP <= 256) {
+    if (ra.k_top > 0) {
+      const bool q = ra.k_top - 1 > 64;
+      const int rc = wsel == 2 ? (q ? launch_select_w<NP, MODE, 2, uint32_t, 2>(ra, BH, stream, plan)
+                                    : launch_select_w<NP, MODE, 2, uint32_t, 1>(ra, BH, stream, plan))
+                               : (q ? launch_select_w<NP, MODE, 4, uint32_t, 2>(ra, BH, stream, plan)
+                                    : launch_select_w<NP, MODE, 4, uint32_t, 1>(ra, BH, stream, plan));
+      if (rc != MXA_OK) return rc;
+      Rows2Args fb = ra;
+      fb.fb_only = 1;
+      return wsel == 2 ? launch_select_w<NP, MODE, 2>(fb, BH, stream, plan) : launch_select_w<NP, MODE, 4>(fb, BH, stream, plan);
+    }
+  }
+  return wsel == 2 ? launch_select_w<NP, MODE, 2>(ra, BH, stream, plan) : launch_select_w<NP, MODE, 4>(ra, BH, stream, plan);
 }
 template <int MODE>
 static int launch_select_m(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
@@ -57,32 +56,22 @@ static int launch_select_m(const Rows2Args& ra, int BH, hipStream_t stream, bool
   if (ra.T <= 256) return launch_select_np<256, MODE>(ra, BH, stream, plan);
   return launch_select_np<512, MODE>(ra, BH, stream, plan);
 }
-// The selection kernel's instantiations are split over three compilations of this
-// file (MXA_SEL_PART 0, 1, 2: build_native.py) so that hipcc builds them in parallel.
+// The selection kernel's instantiations are split over one compilation of this file per
+// score mode (MXA_SEL_PART 1..6; part 0 holds the dispatcher and the standalone top-k:
+// build_native.py) so that hipcc builds them in parallel.
 #ifndef MXA_SEL_PART
 #define MXA_SEL_PART 0
 #endif
 #if MXA_SEL_PART == 0
 int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
-  switch (mode) {
-    case kModeExSign: return launch_select_m<kModeExSign>(ra, BH, stream, plan);
-    case kModeOpExp:
-    case kModeOpMul: return launch_select_p1(ra, mode, BH, stream, plan);
-    default: return launch_select_p2(ra, mode, BH, stream, plan);
-  }
-}
-#elif MXA_SEL_PART == 1
-int launch_select_p1(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
-  return mode == kModeOpMul ? launch_select_m<kModeOpMul>(ra, BH, stream, plan)
-                            : launch_select_m<kModeOpExp>(ra, BH, stream, plan);
+  return launch_select_mode(ra, mode, BH, stream, plan);
 }
 #else
-int launch_select_p2(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan) {
-  switch (mode) {
-    case kModeTrueEx: return launch_select_m<kModeTrueEx>(ra, BH, stream, plan);
-    case kModeElsa: return launch_select_m<kModeElsa>(ra, BH, stream, plan);
-    default: return launch_select_m<kModeTrue>(ra, BH, stream, plan);
-  }
+constexpr int kPartMode[7] = {0, kModeExSign, kModeOpMul, kModeOpExp, kModeTrueEx, kModeElsa, kModeTrue};
+#define MXA_SEL_FN2(i) launch_select_p##i
+#define MXA_SEL_FN(i) MXA_SEL_FN2(i)
+int MXA_SEL_FN(MXA_SEL_PART)(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  return launch_select_m<kPartMode[MXA_SEL_PART]>(ra, BH, stream, plan);
 }
 #endif
 
@@ -125,7 +114,7 @@ extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, i
   const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
   // rows of 513..1024 (PixArt 512x512 self-attention): one wave per row (mxa_topk_wave.hpp);
   // shorter rows: four rows per wave (mxa_topk_grp.hpp, measured faster)
-  if (n > 512 || MXA_SEL_WAVE) {
+  if (n > 512) {
     if (n <= 256) return launch_topk_wave<256>(ga, stream);
     if (n <= 512) return launch_topk_wave<512>(ga, stream);
     return launch_topk_wave<1024>(ga, stream);

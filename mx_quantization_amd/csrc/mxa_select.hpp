@@ -1,20 +1,20 @@
-// Selection kernel: approximate scores + exact-order top-k, FOUR query rows per wave.
+// Selection kernels: approximate scores + exact-order top-k.
 //
 // Per workgroup (one head, a chunk of its query rows): the head's score tables are
-// staged in LDS once (sel_lds):
+// staged in LDS once (sel_lds / sel_stage):
 //   ex_pred        sign words + block exponents
 //   MXINT4 / EXION / partial_*   approximator codes + block scales
 //   true_ex        power-of-two codes + zero indicators + block exponents
 //   ELSA           hash words + the (D+1)-entry cosine table
 //   approx off     MXINT8 codes + exponents (the true scores are ranked)
-// Per wave, four rows at a time, one 16-lane DPP row each:
-//   1. lane gl computes the scores of keys gl, gl + 16, ... into the row's LDS mirror
-//      (exact fp64 block epilogue: the scores are exact sums of integer * 2^e,
-//      SURVEY.md F6), bias added in fp32 as the caller does;
-//   2. grp_topk (mxa_topk_grp.hpp) reproduces torch's CPU topk index order;
-//   3. the k kept indices go out as int64 (the op's idx) and int32 (the finishing
-//      kernel's input), four consecutive rows per wave, and the prune-mask words
-//      when asked for.
+// then per row (sel_scores): the scores (exact fp64 block epilogue where needed: the
+// scores are exact sums of integer * 2^e), bias added in fp32 as the caller
+// does; torch's CPU topk index order; the k kept indices as int64 (the op's idx) and int32
+// (the finishing kernel's input), and the prune-mask words when asked for.
+//   select_kernel<..., uint32_t>  rows of <= 256 keys whose scores pack into 32-bit
+//                     elements (mxa_topk_grp.hpp GEl), then
+//   select_kernel<..., uint64_t>  the rows that do not (fb_only), and every row of the true
+//                     scores, ELSA and rows over 256 keys
 // k_top == 0: scores only (mxa_approx_scores).
 // Callers replaced: the approximator + torch.topk of
 //   workloads/deit/scripts/main.py:101-123, workloads/DiT/models.py:168-194,
@@ -33,17 +33,11 @@ namespace mxa {
 #ifndef MXA_SEL_OCC
 #define MXA_SEL_OCC 4
 #endif
-#ifndef MXA_SELW_OCC
-#define MXA_SELW_OCC 8
-#endif
-// 1: the selection kernel with one wave per query row (select_wave_kernel) -- a tools
-// A/B build; measured slower than four rows per wave (DeiT-base 1.15 vs 0.80 ms: its
-// per-row scalar bookkeeping costs as much issue time as the vector work it saves)
-#ifndef MXA_SEL_WAVE
-#define MXA_SEL_WAVE 0
-#endif
 #ifndef MXA_SEL_SHORT_T
 #define MXA_SEL_SHORT_T 224
+#endif
+#ifndef MXA_SELP_OCC
+#define MXA_SELP_OCC 5  // waves per SIMD the packed pass is compiled for
 #endif
 constexpr int kSelRows = MXA_SEL_ROWS;  // query rows per workgroup (a multiple of 4 * waves)
 // waves per workgroup: 2 for rows of <= 224 keys on a large grid (DeiT-base: 0.97 ->
@@ -219,446 +213,291 @@ __device__ __forceinline__ float elsa_cos_entry(int D, int h) {
   return (float)cos((double)cor);
 }
 
-template <int NP, int MODE, int kSelWaves>
-__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// ---- the head's score tables in LDS (sel_lds) -------------------------------------
+struct SelTabs {
+  int8_t* tcd;    // key codes
+  int16_t* tex;   // key exponents
+  uint32_t* tsg;  // sign / hash words
+  int8_t* tz;     // true_ex zero indicators
+  float* tcs;     // ELSA cosine table
+};
+template <int MODE>
+__device__ __forceinline__ SelTabs sel_stage(const Rows2Args& a, unsigned char* smem, const SelLds& L, int bh) {
   constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
-  const int bh = blockIdx.x;
-  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
-  const int b_ = bh / a.H, h_ = bh % a.H;
-  const SelLds L = sel_lds(MODE, T, D, kst, nbd);
-  int8_t* tcd = reinterpret_cast<int8_t*>(smem + L.cd);    // key codes
-  int16_t* tex = reinterpret_cast<int16_t*>(smem + L.ex);  // key exponents
-  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);  // sign / hash words
-  int8_t* tz = reinterpret_cast<int8_t*>(smem + L.z);      // true_ex zero indicators
-  float* tcs = reinterpret_cast<float*>(smem + L.cs);      // ELSA cosine table
-
-  // ---- stage the head's score tables ----------------------------------------
+  SelTabs t;
+  t.tcd = reinterpret_cast<int8_t*>(smem + L.cd);
+  t.tex = reinterpret_cast<int16_t*>(smem + L.ex);
+  t.tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
+  t.tz = reinterpret_cast<int8_t*>(smem + L.z);
+  t.tcs = reinterpret_cast<float*>(smem + L.cs);
+  const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst;
   const int64_t kb = (int64_t)bh * T;
   if constexpr (MODE == kModeTrue || kOp || MODE == kModeTrueEx) {
     const int8_t* src = MODE == kModeTrue ? a.kc : a.kop;
     const int cpr = a.dpad / 16;
     for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
       const int j = i / cpr, c = i - j * cpr;
-      *reinterpret_cast<uint4*>(tcd + (size_t)j * kst + 16 * c) =
+      *reinterpret_cast<uint4*>(t.tcd + (size_t)j * kst + 16 * c) =
           *reinterpret_cast<const uint4*>(src + (kb + j) * a.dpad + 16 * c);
       if (MODE == kModeTrueEx)
-        *reinterpret_cast<uint4*>(tz + (size_t)j * kst + 16 * c) =
+        *reinterpret_cast<uint4*>(t.tz + (size_t)j * kst + 16 * c) =
             *reinterpret_cast<const uint4*>(a.kz + (kb + j) * a.dpad + 16 * c);
     }
   }
   {
     const int16_t* esrc = MODE == kModeTrue ? a.ksT : a.ksA;
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      if (MODE != kModeElsa) tex[i] = esrc[kb * nbd + i];
-      if (MODE == kModeExSign || MODE == kModeElsa) tsg[i] = a.ksg[kb * nbd + i];
+      if (MODE != kModeElsa) t.tex[i] = esrc[kb * nbd + i];
+      if (MODE == kModeExSign || MODE == kModeElsa) t.tsg[i] = a.ksg[kb * nbd + i];
     }
     if (MODE == kModeElsa)
-      for (int h = threadIdx.x; h <= D; h += blockDim.x) tcs[h] = a.elsa_cos ? a.elsa_cos[h] : elsa_cos_entry(D, h);
+      for (int h = threadIdx.x; h <= D; h += blockDim.x) t.tcs[h] = a.elsa_cos ? a.elsa_cos[h] : elsa_cos_entry(D, h);
   }
   __syncthreads();
-
-  const int npa = grp_alloc(T);
-  const size_t rowb = grp_row_bytes(npa, NP);
-  const GrpRow g = carve_grp(smem + L.rows + (size_t)(4 * wave + gi) * rowb, npa, NP);
-  const int ntw = (T + 31) / 32;  // prune-mask words per row
-  const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
-  for (int rq = (int)blockIdx.y * a.rows_per_wg + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
-    const int r = rq + gi;
-    const bool valid = r < r_end;
-    const int64_t grow = (int64_t)bh * a.N + (valid ? r : rq);
-    const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : rq) * a.bs2 : -1;
-
-    // ---- the row's scores into its mirror ------------------------------------
-#ifdef MXA_SEL_SKIP
-    if (valid && !((MXA_SEL_SKIP) & 2)) {
-#else
-    if (valid) {
-#endif
-      // scores in the score dtype: the approximator GEMM's (or the true matmul's) output
-      // rounded to it, then + bias (MX_transformer_block.py:821-822), rounded again
-      auto emit = [&](int j, float v) {
-        v = round_dt(v, a.s_dt);
-        if (brow >= 0) v = round_dt(v + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
-        if (MODE == kModeTrue) {
-          if (a.true_out) a.true_out[grow * T + j] = v;
-        } else if (a.pred_out) {
-          a.pred_out[grow * T + j] = v;
-        }
-        g.A[j] = pack_ki(order_key(v), (uint32_t)j);
-      };
-      if constexpr (MODE == kModeExSign) {
-        // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
-        uint32_t sq[kMaxNB];
-        int eq[kMaxNB];
-#pragma unroll
-        for (int b = 0; b < kMaxNB; ++b) {
-          sq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
-          eq[b] = b < nbd ? exp_from16(a.qsA[grow * nbd + b]) : 0;
-        }
-        auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
-          constexpr int NBD = decltype(nbd_c)::value;
-          if (brow >= 0 || a.s_dt != kF32) {
-            for (int j = gl; j < T; j += 16) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
-            return;
-          }
-          // no bias: the raw int16 exponents (NaN = INT16_MIN) go straight into the
-          // fast-path test -- a NaN block drives the smallest exponent below -100 --
-          // and a fast-path value (finite, never -0) takes the three-instruction key
-          int eqr[NBD], nbk[NBD];
-#pragma unroll
-          for (int b = 0; b < NBD; ++b) {
-            eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
-            nbk[b] = min(32, D - 32 * b);
-          }
-          float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
-          for (int j = gl; j < T; j += 16) {
-            const int16_t* kex = tex + j * NBD;
-            const uint32_t* ksg = tsg + j * NBD;
-            int e[NBD], m[NBD];
-#pragma unroll
-            for (int b = 0; b < NBD; ++b) {
-              e[b] = eqr[b] + (int)kex[b];
-              m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
-            }
-            int emin = e[0], emax = e[0];
-#pragma unroll
-            for (int b = 1; b < NBD; ++b) {
-              emin = min(emin, e[b]);
-              emax = max(emax, e[b]);
-            }
-            float v;
-            uint32_t key;
-            if (emax - emin <= 23 && emin >= -100) {
-              int sum = 0;
-#pragma unroll
-              for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
-              v = ldexpf((float)sum, emin);
-              const uint32_t u = __float_as_uint(v);
-              key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
-            } else {
-              v = expred_score<NBD>(sq, eq, kex, ksg, D);
-              key = order_key(v);
-            }
-            if (prow) prow[j] = v;
-            g.A[j] = pack_ki(key, (uint32_t)j);
-          }
-        };
-        switch (nbd) {
-          case 1: keys(std::integral_constant<int, 1>{}); break;
-          case 2: keys(std::integral_constant<int, 2>{}); break;
-          case 3: keys(std::integral_constant<int, 3>{}); break;
-          default: keys(std::integral_constant<int, 4>{}); break;
-        }
-      } else if constexpr (MODE == kModeElsa) {
-        // approx = ||MX_K[row r]|| * cos(clamp(pi/D * hamming - 0.127, 0))
-        // (elsa_approximation.py:124-143; the key norm of row r, the reference's broadcast)
-        uint32_t hq[kMaxNB];
-#pragma unroll
-        for (int b = 0; b < kMaxNB; ++b) hq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
-        const float nrm = a.knorm[kb + r];
-        for (int j = gl; j < T; j += 16) {
-          int h = 0;
-#pragma unroll
-          for (int b = 0; b < kMaxNB; ++b)
-            if (b < nbd) h += (int)__popc(hq[b] ^ tsg[j * nbd + b]);
-          emit(j, nrm * tcs[h]);
-        }
-      } else {
-        const int8_t* qsrc = (MODE == kModeTrue ? a.qc : a.qop) + grow * a.dpad;
-        const int16_t* qesrc = (MODE == kModeTrue ? a.qsT : a.qsA) + grow * nbd;
-        uint4 qv[2 * kMaxNB];
-        uint4 qz[MODE == kModeTrueEx ? 2 * kMaxNB : 1];
-        int qe[kMaxNB];
-#pragma unroll
-        for (int b = 0; b < kMaxNB; ++b) {
-          qv[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b) : make_uint4(0, 0, 0, 0);
-          qv[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
-          if constexpr (MODE == kModeTrueEx) {
-            const int8_t* zsrc = a.qz + grow * a.dpad;
-            qz[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b) : make_uint4(0, 0, 0, 0);
-            qz[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
-          }
-          qe[b] = b < nbd ? exp_from16(qesrc[b]) : 0;
-        }
-        for (int j = gl; j < T; j += 16) {
-          bool nan = false;
-          double acc;
-          if constexpr (MODE == kModeTrueEx)
-            acc = g_dot_trueex(qv, qz, qe, nbd, tcd + (size_t)j * kst, tz + (size_t)j * kst, tex + j * nbd, nan);
-          else
-            acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
-          float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
-          // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
-          if (MODE == kModeTrue) v = round_bfloat(round_dt(v, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt) * a.scale;
-          emit(j, v);
-        }
-      }
-    }
-#ifdef MXA_SEL_SKIP  // tools-only phase timing (build_native defines): 2 = scores replaced by hashed keys
-    if ((MXA_SEL_SKIP) & 2)
-      for (int j = gl; j < T; j += 16) g.A[j] = pack_ki(0x80000000u | ((uint32_t)(j * 2654435761u + r * 40503u) >> 26), (uint32_t)j);
-#endif
-    if (k <= 0) continue;  // scores only
-    wave_lds_sync();
-
-    // ---- torch CPU top-k order ------------------------------------------------
-#ifdef MXA_SEL_SKIP  // 1 = no top-k
-    if (!((MXA_SEL_SKIP) & 1))
-#endif
-    grp_topk<NP>(g, T, k, valid, gl);
-
-    // ---- kept indices: four consecutive rows per wave ----------------------------
-    // (measured: per-row stores beat 16-B stores over the four rows' span, whose
-    // per-element LDS gathers cost more VALU and whose HBM writes were larger)
-    if (valid) {
-      for (int p = gl; p < k; p += 16) {
-        const uint32_t ix = (uint32_t)g.A[p];
-        if (a.idx_out) a.idx_out[grow * k + p] = (int64_t)ix;
-        a.idx32[grow * k + p] = (int32_t)ix;
-      }
-    }
-    if (a.mask_out) {  // prune mask: zeros.scatter_(-1, idx, 1) as bits
-      lu32* mw = g.stk;  // free after grp_topk
-      if (gl < ntw) mw[gl] = 0u;
-      wave_lds_sync();
-      if (valid)
-        for (int p = gl; p < k; p += 16) {
-          const uint32_t ix = (uint32_t)g.A[p];
-          atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
-        }
-      wave_lds_sync();
-      if (valid)
-        for (int w = gl; w < ntw; w += 16) a.mask_out[grow * ntw + w] = mw[w];
-    }
-    wave_lds_sync();
-  }
+  return t;
 }
 
-// ---- the selection kernel, ONE WAVE PER QUERY ROW (mxa_topk_wave.hpp) ------------
-// Per workgroup (one head, a chunk of its query rows, kSelWaveW waves): the score
-// tables staged in LDS as above; then each wave takes rows wave, wave + W, ...: lane
-// computes the scores of keys lane, lane + 64, ... into the row's mirror, wave_topk
-// reproduces torch's CPU index order with the row's bookkeeping in scalar registers,
-// and the k kept indices (int64 + int32) and the prune-mask words go out.  The query
-// row's operands are wave-uniform (scalar loads).
-constexpr int kSelWaveW = 4;
-__host__ __device__ inline size_t selw_lds(int mode, int T, int D, int kst, int nbd) {
-  return sel_lds(mode, T, D, kst, nbd).rows + (size_t)kSelWaveW * wrow_bytes(T);
-}
-
-template <int NP, int MODE>
-__global__ __launch_bounds__(64 * kSelWaveW) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : 4, 8))) void select_wave_kernel(Rows2Args a0) {
-  const Rows2Args& a = a0;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr bool kOp = MODE == kModeOpExp || MODE == kModeOpMul;
-  constexpr int EW = NP / 64;
-  const int wave = (int)(threadIdx.x >> 6);
-  const uint32_t lane0 = threadIdx.x & 63;
-  const int bh = blockIdx.x;
+// ---- the approximate (or true) scores of query row r: keys j0, j0 + js, ... -------------
+// sink(j, v, key): v the score as the caller ranks it (score dtype, + bias), key its order
+// key.  pred_out / true_out are written here.
+template <int MODE, typename Sink>
+__device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t, int bh, int r, int j0, int js,
+                                           Sink&& sink) {
   const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const SelLds L = sel_lds(MODE, T, D, kst, nbd);
-  int8_t* tcd = reinterpret_cast<int8_t*>(smem + L.cd);
-  int16_t* tex = reinterpret_cast<int16_t*>(smem + L.ex);
-  uint32_t* tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
-  int8_t* tz = reinterpret_cast<int8_t*>(smem + L.z);
-  float* tcs = reinterpret_cast<float*>(smem + L.cs);
-
-  // ---- stage the head's score tables ----------------------------------------
   const int64_t kb = (int64_t)bh * T;
-  if constexpr (MODE == kModeTrue || kOp || MODE == kModeTrueEx) {
-    const int8_t* src = MODE == kModeTrue ? a.kc : a.kop;
-    const int cpr = a.dpad / 16;
-    for (int i = threadIdx.x; i < T * cpr; i += blockDim.x) {
-      const int j = i / cpr, c = i - j * cpr;
-      *reinterpret_cast<uint4*>(tcd + (size_t)j * kst + 16 * c) =
-          *reinterpret_cast<const uint4*>(src + (kb + j) * a.dpad + 16 * c);
-      if (MODE == kModeTrueEx)
-        *reinterpret_cast<uint4*>(tz + (size_t)j * kst + 16 * c) =
-            *reinterpret_cast<const uint4*>(a.kz + (kb + j) * a.dpad + 16 * c);
+  const int64_t grow = (int64_t)bh * a.N + r;
+  const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : -1;
+  // scores in the score dtype: the approximator GEMM's (or the true matmul's) output
+  // rounded to it, then + bias (MX_transformer_block.py:821-822), rounded again
+  auto emit = [&](int j, float v) {
+    v = round_dt(v, a.s_dt);
+    if (brow >= 0) v = round_dt(v + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
+    if (MODE == kModeTrue) {
+      if (a.true_out) a.true_out[grow * T + j] = v;
+    } else if (a.pred_out) {
+      a.pred_out[grow * T + j] = v;
     }
-  }
-  {
-    const int16_t* esrc = MODE == kModeTrue ? a.ksT : a.ksA;
-    for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      if (MODE != kModeElsa) tex[i] = esrc[kb * nbd + i];
-      if (MODE == kModeExSign || MODE == kModeElsa) tsg[i] = a.ksg[kb * nbd + i];
-    }
-    if (MODE == kModeElsa)
-      for (int h = threadIdx.x; h <= D; h += blockDim.x) tcs[h] = a.elsa_cos ? a.elsa_cos[h] : elsa_cos_entry(D, h);
-  }
-  __syncthreads();
-
-  const WRow g = carve_wrow(smem + L.rows + (size_t)wave * wrow_bytes(T), T);
-  const int ntw = (T + 31) / 32;  // prune-mask words per row
-  const int r_end = min(a.N, (int)(blockIdx.y + 1) * a.rows_per_wg);
-  for (int r = (int)blockIdx.y * a.rows_per_wg + wave; r < r_end; r += kSelWaveW) {
-    // the argument block re-read per row (scalar loads, cache hits) rather than held in
-    // SGPRs across the top-k: SGPRs bound the resident waves
-    typedef __attribute__((address_space(4))) const Rows2Args KArgs;
-    KArgs* ap = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ap));
-    KArgs& a = *ap;
-    uint32_t lane = lane0;  // (re-derived per row as well: its hoisted address arithmetic spilled)
-    asm volatile("" : "+v"(lane));
-    // (every size re-read too: hoisted, the top-k's conditions on k and T were spilled)
-    const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst, k = a.k_top;
-    const int64_t kb = (int64_t)bh * T;
-    const int64_t grow = (int64_t)bh * a.N + r;
-    const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)r * a.bs2 : -1;
-
-    // ---- the row's scores into its mirror ------------------------------------
-    auto emit = [&](int j, float v) {
-      v = round_dt(v, a.s_dt);
-      if (brow >= 0) v = round_dt(v + load_dt(a.bias, brow + (int64_t)j * a.bs3, a.in_dt), a.s_dt);
-      if (MODE == kModeTrue) {
-        if (a.true_out) a.true_out[grow * T + j] = v;
-      } else if (a.pred_out) {
-        a.pred_out[grow * T + j] = v;
-      }
-      g.A[j] = pack_ki(order_key(v), (uint32_t)j);
-    };
-    if constexpr (MODE == kModeExSign) {
-      // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
-      uint32_t sq[kMaxNB];
-      int eq[kMaxNB];
+    sink(j, v, order_key(v));
+  };
+  if constexpr (MODE == kModeExSign) {
+    // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
+    uint32_t sq[kMaxNB];
+    int eq[kMaxNB];
 #pragma unroll
-      for (int b = 0; b < kMaxNB; ++b) {
-        sq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
-        eq[b] = b < nbd ? s_exp16(a.qsA, grow * nbd + b) : 0;
+    for (int b = 0; b < kMaxNB; ++b) {
+      sq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
+      eq[b] = b < nbd ? exp_from16(a.qsA[grow * nbd + b]) : 0;
+    }
+    auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
+      constexpr int NBD = decltype(nbd_c)::value;
+      if (brow >= 0 || a.s_dt != kF32) {
+        for (int j = j0; j < T; j += js) emit(j, expred_score<NBD>(sq, eq, t.tex + j * NBD, t.tsg + j * NBD, D));
+        return;
       }
-      auto keys = [&](auto nbd_c) {
-        constexpr int NBD = decltype(nbd_c)::value;
-        if (brow >= 0 || a.s_dt != kF32) {
-          for (int j = (int)lane; j < T; j += 64) emit(j, expred_score<NBD>(sq, eq, tex + j * NBD, tsg + j * NBD, D));
-          return;
-        }
-        int eqr[NBD], nbk[NBD];
+      // no bias: the raw int16 exponents (NaN = INT16_MIN) go straight into the
+      // fast-path test -- a NaN block drives the smallest exponent below -100 --
+      // and a fast-path value (finite, never -0) takes the three-instruction key
+      int eqr[NBD], nbk[NBD];
+#pragma unroll
+      for (int b = 0; b < NBD; ++b) {
+        eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
+        nbk[b] = min(32, D - 32 * b);
+      }
+      float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
+      for (int j = j0; j < T; j += js) {
+        const int16_t* kex = t.tex + j * NBD;
+        const uint32_t* ksg = t.tsg + j * NBD;
+        int e[NBD], m[NBD];
 #pragma unroll
         for (int b = 0; b < NBD; ++b) {
-          eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
-          nbk[b] = min(32, D - 32 * b);
+          e[b] = eqr[b] + (int)kex[b];
+          m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
         }
-        float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
-        // the common case branch-free (exponent spread <= 23, smallest >= -100: the exact
-        // int32 sum, one rounding); rows with any other key (NaN blocks, wide spreads)
-        // get a second pass over the flagged keys with the exact fp64 sum
-        uint64_t anyslow = 0;
-        for (int j = (int)lane; j < T; j += 64) {
-          const int16_t* kex = tex + j * NBD;
-          const uint32_t* ksg = tsg + j * NBD;
-          int e[NBD], m[NBD];
+        int emin = e[0], emax = e[0];
 #pragma unroll
-          for (int b = 0; b < NBD; ++b) {
-            e[b] = eqr[b] + (int)kex[b];
-            m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
-          }
-          int emin = e[0], emax = e[0];
-#pragma unroll
-          for (int b = 1; b < NBD; ++b) {
-            emin = min(emin, e[b]);
-            emax = max(emax, e[b]);
-          }
+        for (int b = 1; b < NBD; ++b) {
+          emin = min(emin, e[b]);
+          emax = max(emax, e[b]);
+        }
+        float v;
+        uint32_t key;
+        if (emax - emin <= 23 && emin >= -100) {
           int sum = 0;
 #pragma unroll
-          for (int b = 0; b < NBD; ++b) sum += m[b] << ((e[b] - emin) & 31);
-          const float v = ldexpf((float)sum, emin);
+          for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
+          v = ldexpf((float)sum, emin);
           const uint32_t u = __float_as_uint(v);
-          anyslow |= w_ballot(!(emax - emin <= 23 && emin >= -100));
-          if (prow) prow[j] = v;
-          g.A[j] = pack_ki(u ^ ((uint32_t)((int)u >> 31) | 0x80000000u), (uint32_t)j);
+          key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
+        } else {
+          v = expred_score<NBD>(sq, eq, kex, ksg, D);
+          key = order_key(v);
         }
-        if (anyslow) {
-          for (int j = (int)lane; j < T; j += 64) {
-            const int16_t* kex = tex + j * NBD;
-            int emin = 1 << 20, emax = -(1 << 20);
-#pragma unroll
-            for (int b = 0; b < NBD; ++b) {
-              emin = min(emin, eqr[b] + (int)kex[b]);
-              emax = max(emax, eqr[b] + (int)kex[b]);
-            }
-            if (!(emax - emin <= 23 && emin >= -100)) {
-              const float v = expred_score<NBD>(sq, eq, kex, tsg + j * NBD, D);
-              if (prow) prow[j] = v;
-              g.A[j] = pack_ki(order_key(v), (uint32_t)j);
-            }
-          }
-        }
-      };
-      switch (nbd) {
-        case 1: keys(std::integral_constant<int, 1>{}); break;
-        case 2: keys(std::integral_constant<int, 2>{}); break;
-        case 3: keys(std::integral_constant<int, 3>{}); break;
-        default: keys(std::integral_constant<int, 4>{}); break;
+        if (prow) prow[j] = v;
+        sink(j, v, key);
       }
-    } else if constexpr (MODE == kModeElsa) {
-      uint32_t hq[kMaxNB];
-#pragma unroll
-      for (int b = 0; b < kMaxNB; ++b) hq[b] = b < nbd ? ((cu32)(a.qsg + grow * nbd))[b] : 0u;
-      const float nrm = a.knorm[kb + r];
-      for (int j = (int)lane; j < T; j += 64) {
-        int h = 0;
-#pragma unroll
-        for (int b = 0; b < kMaxNB; ++b)
-          if (b < nbd) h += (int)__popc(hq[b] ^ tsg[j * nbd + b]);
-        emit(j, nrm * tcs[h]);
-      }
-    } else {
-      const int8_t* qsrc = (MODE == kModeTrue ? a.qc : a.qop) + grow * a.dpad;
-      const int16_t* qesrc = MODE == kModeTrue ? a.qsT : a.qsA;
-      uint4 qv[2 * kMaxNB];
-      uint4 qz[MODE == kModeTrueEx ? 2 * kMaxNB : 1];
-      int qe[kMaxNB];
-#pragma unroll
-      for (int b = 0; b < kMaxNB; ++b) {
-        const cu32 qw = (cu32)(qsrc + 32 * b);
-        qv[2 * b] = b < nbd ? make_uint4(qw[0], qw[1], qw[2], qw[3]) : make_uint4(0, 0, 0, 0);
-        qv[2 * b + 1] = b < nbd ? make_uint4(qw[4], qw[5], qw[6], qw[7]) : make_uint4(0, 0, 0, 0);
-        if constexpr (MODE == kModeTrueEx) {
-          const cu32 zw = (cu32)(a.qz + grow * a.dpad + 32 * b);
-          qz[2 * b] = b < nbd ? make_uint4(zw[0], zw[1], zw[2], zw[3]) : make_uint4(0, 0, 0, 0);
-          qz[2 * b + 1] = b < nbd ? make_uint4(zw[4], zw[5], zw[6], zw[7]) : make_uint4(0, 0, 0, 0);
-        }
-        qe[b] = b < nbd ? s_exp16(qesrc, grow * nbd + b) : 0;
-      }
-      for (int j = (int)lane; j < T; j += 64) {
-        bool nan = false;
-        double acc;
-        if constexpr (MODE == kModeTrueEx)
-          acc = g_dot_trueex(qv, qz, qe, nbd, tcd + (size_t)j * kst, tz + (size_t)j * kst, tex + j * nbd, nan);
-        else
-          acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, tcd + (size_t)j * kst, tex + j * nbd, nan);
-        float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
-        if (MODE == kModeTrue) v = round_bfloat(round_dt(v, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt) * a.scale;
-        emit(j, v);
-      }
+    };
+    switch (nbd) {
+      case 1: keys(std::integral_constant<int, 1>{}); break;
+      case 2: keys(std::integral_constant<int, 2>{}); break;
+      case 3: keys(std::integral_constant<int, 3>{}); break;
+      default: keys(std::integral_constant<int, 4>{}); break;
     }
-    if (k <= 0) continue;  // scores only
-    wave_lds_sync();
+  } else if constexpr (MODE == kModeElsa) {
+    // approx = ||MX_K[row r]|| * cos(clamp(pi/D * hamming - 0.127, 0))
+    // (elsa_approximation.py:124-143; the key norm of row r, the reference's broadcast)
+    uint32_t hq[kMaxNB];
+#pragma unroll
+    for (int b = 0; b < kMaxNB; ++b) hq[b] = b < nbd ? a.qsg[grow * nbd + b] : 0u;
+    const float nrm = a.knorm[kb + r];
+    for (int j = j0; j < T; j += js) {
+      int h = 0;
+#pragma unroll
+      for (int b = 0; b < kMaxNB; ++b)
+        if (b < nbd) h += (int)__popc(hq[b] ^ t.tsg[j * nbd + b]);
+      emit(j, nrm * t.tcs[h]);
+    }
+  } else {
+    const int8_t* qsrc = (MODE == kModeTrue ? a.qc : a.qop) + grow * a.dpad;
+    const int16_t* qesrc = (MODE == kModeTrue ? a.qsT : a.qsA) + grow * nbd;
+    uint4 qv[2 * kMaxNB];
+    uint4 qz[MODE == kModeTrueEx ? 2 * kMaxNB : 1];
+    int qe[kMaxNB];
+#pragma unroll
+    for (int b = 0; b < kMaxNB; ++b) {
+      qv[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b) : make_uint4(0, 0, 0, 0);
+      qv[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
+      if constexpr (MODE == kModeTrueEx) {
+        const int8_t* zsrc = a.qz + grow * a.dpad;
+        qz[2 * b] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b) : make_uint4(0, 0, 0, 0);
+        qz[2 * b + 1] = b < nbd ? *reinterpret_cast<const uint4*>(zsrc + 32 * b + 16) : make_uint4(0, 0, 0, 0);
+      }
+      qe[b] = b < nbd ? exp_from16(qesrc[b]) : 0;
+    }
+    for (int j = j0; j < T; j += js) {
+      bool nan = false;
+      double acc;
+      if constexpr (MODE == kModeTrueEx)
+        acc = g_dot_trueex(qv, qz, qe, nbd, t.tcd + (size_t)j * kst, t.tz + (size_t)j * kst, t.tex + j * nbd, nan);
+      else
+        acc = g_dot<MODE == kModeOpMul>(qv, qe, nbd, t.tcd + (size_t)j * kst, t.tex + j * nbd, nan);
+      float v = nan ? __uint_as_float(0x7FC00000u) : (float)acc;
+      // true = quantize_elemwise(fl32(QK^T)) * scale   (matmul.py:88-91, caller)
+      if (MODE == kModeTrue) v = round_bfloat(round_dt(v, a.s_dt), a.bfloat, kRoundNearest, 1, a.s_dt) * a.scale;
+      emit(j, v);
+    }
+  }
+}
 
-    // ---- torch CPU top-k order ------------------------------------------------
-    wave_topk<EW>(g, T, k);
+// prune mask words of one row from its kept indices (zeros.scatter_(-1, idx, 1) as bits):
+// idx_at(p) for p = p0, p0 + ps, ... < k; mw is a per-row LDS scratch of ntw words
+template <typename IdxAt>
+__device__ __forceinline__ void sel_mask_words(const Rows2Args& a, __attribute__((address_space(3))) uint32_t* mw,
+                                               int64_t grow, bool valid, int p0, int ps, int k, IdxAt&& idx_at) {
+  const int ntw = (a.T + 31) / 32;
+  for (int w = p0; w < ntw; w += ps) mw[w] = 0u;
+  wave_lds_sync();
+  if (valid)
+    for (int p = p0; p < k; p += ps) {
+      const uint32_t ix = idx_at(p);
+      atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
+    }
+  wave_lds_sync();
+  if (valid)
+    for (int w = p0; w < ntw; w += ps) a.mask_out[grow * ntw + w] = mw[w];
+}
 
-    // ---- kept indices, prune mask ----------------------------------------------
-    for (int p = (int)lane; p < k; p += 64) {
-      const uint32_t ix = (uint32_t)g.A[p];
+// ---- four query rows per wave (mxa_topk_grp.hpp) ---------------------------------
+// rows rq + (lane >> 4) of head bh; g0 = the wave's per-row areas (grp_row_bytes each).
+// El = uint64_t: any row (a.fb_only: only the rows the packed pass left, idx32[row][0] < 0).
+// El = uint32_t (packed): a row whose scores do not all leave the key's low byte free is
+// left for the 64-bit pass: idx32[row][0] = -1.
+template <int NP, int MODE, typename El, int QM>
+__device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, unsigned char* g0, int bh, int rq,
+                                          int r_end, int lane) {
+  constexpr bool kPacked = sizeof(El) == 4;
+  const int gi = lane >> 4, gl = lane & 15;
+  const int T = a.T, k = a.k_top;
+  const int npa = grp_alloc(T);
+  const GrpRow<El> g = carve_grp<El>(g0 + (size_t)gi * grp_row_bytes(npa, NP, sizeof(El)), npa, NP);
+  const int r = rq + gi;
+  bool valid = r < r_end;
+  const int64_t grow = (int64_t)bh * a.N + (valid ? r : rq);
+  if (!kPacked && a.fb_only && valid) valid = a.idx32[grow * k] < 0;
+  uint32_t bad = 0u;
+#ifdef MXA_SEL_SKIP
+  if (valid && !((MXA_SEL_SKIP) & 2))
+#else
+  if (valid)
+#endif
+  {
+    if constexpr (kPacked)
+      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float v, uint32_t key) {
+        bad |= q_bad_bits(v);
+        g.A[j] = qelem(key, (uint32_t)j);
+      });
+    else
+      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float, uint32_t key) { g.A[j] = pack_ki(key, (uint32_t)j); });
+  }
+#ifdef MXA_SEL_SKIP  // tools-only phase timing (build_native defines): 2 = scores replaced by hashed keys
+  if ((MXA_SEL_SKIP) & 2)
+    for (int j = gl; j < T; j += 16) {
+      const uint32_t key = 0x80000000u | ((uint32_t)(j * 2654435761u + r * 40503u) >> 26 << 8);
+      if constexpr (kPacked) g.A[j] = qelem(key, (uint32_t)j);
+      else g.A[j] = pack_ki(key, (uint32_t)j);
+    }
+#endif
+  if (k <= 0) return;  // scores only
+  if constexpr (kPacked) {  // this row's 16 lanes: any score that does not pack
+    const uint64_t bw = __builtin_amdgcn_ballot_w64(bad != 0u);
+    if (valid && ((bw >> (16 * gi)) & 0xFFFFull) != 0) {
+      if (gl == 0) a.idx32[grow * k] = -1;
+      valid = false;
+    }
+  }
+  wave_lds_sync();
+#ifdef MXA_SEL_SKIP  // 1 = no top-k
+  if (!((MXA_SEL_SKIP) & 1))
+#endif
+  grp_topk<NP, El, QM>(g, T, k, valid, gl);
+  // kept indices: four consecutive rows per wave
+  if (valid) {
+    for (int p = gl; p < k; p += 16) {
+      const uint32_t ix = GEl<El>::idx(g.A[p]);
       if (a.idx_out) a.idx_out[grow * k + p] = (int64_t)ix;
       a.idx32[grow * k + p] = (int32_t)ix;
     }
-    if (a.mask_out) {  // prune mask: zeros.scatter_(-1, idx, 1) as bits
-      wl32* mw = (wl32*)g.SL;  // free after the top-k
-      if ((int)lane < ntw) mw[lane] = 0u;
-      wave_lds_sync();
-      for (int p = (int)lane; p < k; p += 64) {
-        const uint32_t ix = (uint32_t)g.A[p];
-        atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
-      }
-      wave_lds_sync();
-      if ((int)lane < ntw) a.mask_out[grow * ntw + lane] = mw[lane];
+  }
+  if (a.mask_out) sel_mask_words(a, g.stk, grow, valid, gl, 16, k, [&](int p) { return GEl<El>::idx(g.A[p]); });
+  wave_lds_sync();
+}
+
+// Selection kernel, four query rows per wave.  El = uint64_t: rows of up to 512 keys,
+// every approximator (a.fb_only: only the rows the packed pass left; a workgroup
+// without such rows returns at once).  El = uint32_t: the packed pass (rows of <= 256
+// keys; half the LDS per row, so more resident waves).
+template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0>
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? MXA_SELP_OCC : NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x;
+  const int r0 = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r0 + a.rows_per_wg);
+  if (sizeof(El) == 8 && a.fb_only) {
+    int any = 0;
+    for (int r = r0 + (int)threadIdx.x; r < r_end; r += blockDim.x)
+      any |= a.idx32[((int64_t)bh * a.N + r) * a.k_top] < 0;
+    if (!__syncthreads_or(any)) return;
+  }
+  const SelLds L = sel_lds(MODE, a.T, a.D, a.kst, a.nbd);
+  const SelTabs t = sel_stage<MODE>(a, smem, L, bh);
+  unsigned char* g0 = smem + L.rows + (size_t)4 * wave * grp_row_bytes(grp_alloc(a.T), NP, sizeof(El));
+  for (int rq = r0 + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
+    if (sizeof(El) == 8 && a.fb_only) {  // the rows of this group that are left
+      const int r = min(rq + (lane >> 4), r_end - 1);
+      if (__builtin_amdgcn_ballot_w64(rq + (lane >> 4) < r_end && a.idx32[((int64_t)bh * a.N + r) * a.k_top] < 0) == 0)
+        continue;
     }
-    wave_lds_sync();
+    sel_rows4<NP, MODE, El, QM>(a, t, g0, bh, rq, r_end, lane);
   }
 }
 
@@ -680,7 +519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
   const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * 4 + gi;
   const bool valid = row < a.rows;
   const int npa = grp_alloc(a.n);
-  const GrpRow g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
+  const GrpRow<> g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
   const int64_t src = (valid ? row : 0) * a.ld;
   if (valid)
     for (int j = gl; j < a.n; j += 16) g.A[j] = pack_ki(order_key(load_dt(a.vals, src + j, a.dt)), (uint32_t)j);
@@ -712,7 +551,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
 // one wave per row (mxa_topk_wave.hpp): waves of a 256-thread workgroup take rows
 // 4 blockIdx.x + wave
 template <int NP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? MXA_SELW_OCC : NP <= 512 ? 4 : 2, 8))) void topk_wave_kernel(GrpTopkArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 8 : NP <= 512 ? 4 : 2, 8))) void topk_wave_kernel(GrpTopkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = (int)(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;

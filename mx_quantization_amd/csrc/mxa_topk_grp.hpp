@@ -25,6 +25,13 @@
 // wave-wide step.  The row itself lives in an LDS mirror A (order key << 32 | index);
 // swaps publish their positions in P, then the pairs trade elements.
 //
+// Elements: El = uint64_t, (order key << 32) | index, for any row; or El = uint32_t, the
+// packed form (order key & 0xFFFFFF00) | index for rows of <= 256 keys whose scores all
+// have a zero low mantissa byte (then the key's low byte is 0x00 / 0xFF and carries no
+// order; the approximate scores of ex_pred / MXINT4 / EXION / partial / true_ex are such
+// sums of a few small integers times powers of two): half the LDS per row and 32-bit
+// compares, key(a) > key(b) <=> a > (b | 0xFF) (GEl below).
+//
 // std::sort's final insertion sort is a stable sort of the arrangement the introsort
 // loop leaves; because those segments are mutually ordered it equals a stable sort of
 // each <= 16-element segment (or of the whole prefix when k-1 <= 64), computed as a
@@ -34,12 +41,6 @@
 #include "mxa_order.hpp"
 
 namespace mxa {
-
-#ifndef MXA_GRP_ELEM_X
-// 1: 32-position windows exchange whole elements instead of positions (one LDS round trip
-// fewer per step); measured neutral at DeiT-base / DiT (0.803 vs 0.795, 1.170 vs 1.176 ms)
-#define MXA_GRP_ELEM_X 0
-#endif
 
 typedef __attribute__((address_space(3))) uint32_t lu32;
 typedef __attribute__((address_space(3))) uint16_t lu16;
@@ -54,38 +55,63 @@ constexpr int kGSeg = 16;  // final sort segments queued for one ranking pass
 // width and the swap-rank split HP = NP/2) and the mirror's allocated positions NPA
 // (runtime: T rounded up to a window width, so that the LDS per row -- and with it
 // the resident waves -- follows the row length)
-// per-row LDS: mirror A[NPA] (u64), exchange slots P[NP] + 16 trash slots (u8 for
+// per-row LDS: mirror A[NPA] (El), exchange slots P[NP] + 16 trash slots (u8 for
 // NP <= 256, else u16), introsort stack, queue of final segments
 __host__ __device__ constexpr int grp_pbytes(int NP) { return ((NP <= 256 ? 1 : 2) * (NP + 16) + 15) & ~15; }
-__host__ __device__ constexpr size_t grp_row_bytes(int NPA, int NP) {
-  return (size_t)8 * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg;
+__host__ __device__ constexpr size_t grp_row_bytes(int NPA, int NP, int elb = 8) {
+  return (size_t)elb * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg;
 }
 // (the window widths 16 E are 32, 64, ..., 256, 384, 512, so NPA is one of them)
 __host__ __device__ constexpr int grp_alloc(int T) { return T <= 256 ? (T + 31) & ~31 : (T <= 384 ? 384 : 512); }
 
+// element traits: key for the stop compares, order, index
+template <typename El>
+struct GEl;
+template <>
+struct GEl<uint64_t> {
+  typedef __attribute__((address_space(3))) uint64_t LT;
+  __device__ static uint32_t key(uint64_t x) { return (uint32_t)(x >> 32); }
+  __device__ static bool gt(uint64_t a, uint64_t b) { return key(a) > key(b); }
+  __device__ static uint32_t thr_le(uint32_t pk) { return pk; }  // key(x) <= p  <=>  key(x) <= thr_le
+  __device__ static uint32_t thr_ge(uint32_t pk) { return pk; }  // key(x) >= p  <=>  key(x) >= thr_ge
+  __device__ static uint32_t idx(uint64_t x) { return (uint32_t)x; }
+};
+template <>
+struct GEl<uint32_t> {
+  typedef __attribute__((address_space(3))) uint32_t LT;
+  __device__ static uint32_t key(uint32_t x) { return x; }
+  __device__ static bool gt(uint32_t a, uint32_t b) { return a > (b | 0xFFu); }
+  __device__ static uint32_t thr_le(uint32_t pk) { return pk | 0xFFu; }
+  __device__ static uint32_t thr_ge(uint32_t pk) { return pk & ~0xFFu; }
+  __device__ static uint32_t idx(uint32_t x) { return x & 0xFFu; }
+};
+
+template <typename El = uint64_t>
 struct GrpRow {
-  lu64* A;
+  typename GEl<El>::LT* A;
   unsigned char __attribute__((address_space(3)))* P;
   lu32* stk;
   lu32* seg;
   int npa;  // allocated mirror positions
 };
-__device__ __forceinline__ GrpRow carve_grp(unsigned char* base, int npa, int NP) {
-  GrpRow g;
-  g.A = (lu64*)(lu32*)(base);
-  g.P = (unsigned char __attribute__((address_space(3)))*)(base + 8 * npa);
-  g.stk = (lu32*)(base + 8 * npa + grp_pbytes(NP));
-  g.seg = (lu32*)(base + 8 * npa + grp_pbytes(NP) + 4 * kGStk);
+template <typename El = uint64_t>
+__device__ __forceinline__ GrpRow<El> carve_grp(unsigned char* base, int npa, int NP) {
+  GrpRow<El> g;
+  constexpr int B = (int)sizeof(El);
+  g.A = (typename GEl<El>::LT*)(lu32*)(base);
+  g.P = (unsigned char __attribute__((address_space(3)))*)(base + B * npa);
+  g.stk = (lu32*)(base + B * npa + grp_pbytes(NP));
+  g.seg = (lu32*)(base + B * npa + grp_pbytes(NP) + 4 * kGStk);
   g.npa = npa;
   return g;
 }
-template <int NP>
-__device__ __forceinline__ void p_put(const GrpRow& g, uint32_t i, uint32_t v) {
+template <int NP, typename El>
+__device__ __forceinline__ void p_put(const GrpRow<El>& g, uint32_t i, uint32_t v) {
   if constexpr (NP <= 256) ((lu8*)g.P)[i] = (uint8_t)v;
   else ((lu16*)g.P)[i] = (uint16_t)v;
 }
-template <int NP>
-__device__ __forceinline__ uint32_t p_get(const GrpRow& g, uint32_t i) {
+template <int NP, typename El>
+__device__ __forceinline__ uint32_t p_get(const GrpRow<El>& g, uint32_t i) {
   if constexpr (NP <= 256) return ((lu8*)g.P)[i];
   else return ((lu16*)g.P)[i];
 }
@@ -99,27 +125,33 @@ __device__ __forceinline__ uint32_t g_shl_le(uint32_t acc, uint32_t a, uint32_t 
   asm("v_cmp_le_u32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
   return acc;
 }
-// the stop masks of two positions at once: L = 4 L + 2 (k0 <= p) + (k1 <= p),
-// R = 4 R + 2 (p <= k0) + (p <= k1).  The four compares go to four SGPR pairs first,
-// so each add-with-carry reads a carry written three instructions earlier: no wait
-// states (one compare + add-with-carry pair at a time needs an s_nop between them)
-__device__ __forceinline__ void g_stops2(uint32_t& L, uint32_t& R, uint32_t k0, uint32_t k1, uint32_t p) {
+// the stop masks of two positions at once: L = 4 L + 2 (k0 <= pl) + (k1 <= pl),
+// R = 4 R + 2 (pr <= k0) + (pr <= k1) (pl = pr = p on 64-bit elements; the packed ones
+// compare against p | 0xFF and p & ~0xFF).  The four compares go to four SGPR pairs
+// first, so each add-with-carry reads a carry written three instructions earlier: no
+// wait states (one compare + add-with-carry pair at a time needs an s_nop between them)
+__device__ __forceinline__ void g_stops2(uint32_t& L, uint32_t& R, uint32_t k0, uint32_t k1, uint32_t pl, uint32_t pr) {
   uint64_t c0, c1, c2, c3;
   asm("v_cmp_le_u32_e64 %2, %6, %8\n\t"
-      "v_cmp_le_u32_e64 %3, %8, %6\n\t"
+      "v_cmp_le_u32_e64 %3, %9, %6\n\t"
       "v_cmp_le_u32_e64 %4, %7, %8\n\t"
-      "v_cmp_le_u32_e64 %5, %8, %7\n\t"
+      "v_cmp_le_u32_e64 %5, %9, %7\n\t"
       "v_addc_co_u32_e64 %0, %2, %0, %0, %2\n\t"
       "v_addc_co_u32_e64 %1, %3, %1, %1, %3\n\t"
       "v_addc_co_u32_e64 %0, %4, %0, %0, %4\n\t"
       "v_addc_co_u32_e64 %1, %5, %1, %1, %5"
       : "+v"(L), "+v"(R), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
-      : "v"(k0), "v"(k1), "v"(p));
+      : "v"(k0), "v"(k1), "v"(pl), "v"(pr));
 }
 
 // r + (a > b) for 64-bit a, b: a compare and an add-with-carry
 __device__ __forceinline__ uint32_t g_add_gt(uint32_t r, uint64_t a, uint64_t b) {
   asm("v_cmp_gt_u64 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, 0, vcc" : "+v"(r) : "v"(a), "v"(b) : "vcc");
+  return r;
+}
+// r + (a > b) for 32-bit a, b
+__device__ __forceinline__ uint32_t g_add_gt32(uint32_t r, uint32_t a, uint32_t b) {
+  asm("v_cmp_gt_u32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, 0, vcc" : "+v"(r) : "v"(a), "v"(b) : "vcc");
   return r;
 }
 // ri += (kj > ki), rj -= (kj > ki): one compare, an add-with-carry and a
@@ -159,8 +191,9 @@ constexpr int pow2_floor() { return E >= 32 ? 32 : E >= 16 ? 16 : E >= 8 ? 8 : E
 // the wave with act set (l - f >= 4), all rows in lockstep.  Window: lane gl holds
 // positions lb + e, lb = b + E*gl, e < E (b even, b <= f, l <= b + 16E <= NPA).
 // HP = NP / 2 (>= any swap count).  Returns the cut.
-template <int E, int NP>
-__device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int b, bool act, int gl) {
+template <int E, int NP, typename El>
+__device__ __forceinline__ int grp_partition(const GrpRow<El>& g, int f, int l, int b, bool act, int gl) {
+  using T = GEl<El>;
   static_assert(E % 2 == 0, "window widths are even");
   constexpr int HP = NP / 2;
   const int fa = act ? f : 0, la = act ? l : 4;  // idle rows read harmless positions
@@ -169,28 +202,32 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // the median candidates (whole elements) and the window, all in one LDS round trip:
   // the median's iter_swap is applied to the stop masks in registers and written back
   // while the masks are formed (position f is never a stop; position m holds old f)
-  const uint64_t xf = g.A[fa], xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1];
-  uint32_t K[E], I2[2];
+  const El xf = g.A[fa], xa = g.A[fa + 1], xb = g.A[mid], xc = g.A[la - 1];
+  uint32_t K[E];  // the window's keys (packed elements: the elements)
 #pragma unroll
   for (int e = 0; e < E; e += 2) {
-    const u32x4 v = *(const lu128*)(g.A + lb + e);
-    K[e] = v.y;
-    K[e + 1] = v.w;
-    if (E == 2) I2[0] = v.x, I2[1] = v.z;  // whole elements: the exchange below moves them
+    if constexpr (sizeof(El) == 8) {
+      const u32x4 v = *(const lu128*)(g.A + lb + e);
+      K[e] = v.y;
+      K[e + 1] = v.w;
+    } else {
+      const uint64_t v = *(const __attribute__((address_space(3))) uint64_t*)(g.A + lb + e);
+      K[e] = (uint32_t)v;
+      K[e + 1] = (uint32_t)(v >> 32);
+    }
   }
-  const uint32_t ka = hi32(xa), kb = hi32(xb), kc = hi32(xc);
   // __move_median_to_first(f, f+1, mid, l-1) with cmp = greater, branch-free:
   //   a>b: (b>c ? mid : a>c ? l-1 : f+1);  else: (a>c ? f+1 : b>c ? l-1 : mid)
-  const uint32_t ab = ka > kb, bc = kb > kc, ac = ka > kc;
+  const uint32_t ab = T::gt(xa, xb), bc = T::gt(xb, xc), ac = T::gt(xa, xc);
   const uint32_t pick_b = (ab & bc) | (~ab & ~ac & ~bc & 1u);
   const uint32_t pick_c = (ab & ~bc & ac) | (~ab & ~ac & bc & 1u);
   int m = fa + 1;
-  uint64_t xm = xa;
+  El xm = xa;
   m = pick_c ? la - 1 : m;
   xm = pick_c ? xc : xm;
   m = pick_b ? mid : m;
   xm = pick_b ? xb : xm;
-  const uint32_t p = hi32(xm), kf = hi32(xf);
+  const uint32_t pl = T::thr_le(T::key(xm)), pr = T::thr_ge(T::key(xm)), kf = T::key(xf);
   if (act) {  // iter_swap(f, median)
     g.A[f] = xm;
     g.A[m] = xf;
@@ -198,12 +235,12 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // stop masks, bit (E-1-e) <-> position lb + e
   uint32_t Lm = 0, Rm = 0;
 #pragma unroll
-  for (int e = 0; e < E; e += 2) g_stops2(Lm, Rm, K[e], K[e + 1], p);
+  for (int e = 0; e < E; e += 2) g_stops2(Lm, Rm, K[e], K[e + 1], pl, pr);
   {  // position m now holds old f (key kf)
     const int em = m - lb;
     const uint32_t bm = (uint32_t)em < (uint32_t)E ? 1u << (E - 1 - em) : 0u;
-    Lm = (Lm & ~bm) | (kf <= p ? bm : 0u);
-    Rm = (Rm & ~bm) | (p <= kf ? bm : 0u);
+    Lm = (Lm & ~bm) | (kf <= pl ? bm : 0u);
+    Rm = (Rm & ~bm) | (pr <= kf ? bm : 0u);
   }
   const int lo = min(max(f + 1 - lb, 0), E), hi = min(max(l - lb, 0), E);
   const uint32_t rng = act ? (lowbits(E - lo) & ~lowbits(E - hi)) : 0u;
@@ -235,34 +272,6 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   // row at a time (only the swaps move: ~range/4 of the positions)
   // (u8 slots: the slot values are LDS byte addresses, the base folded into the
   // popcount accumulations)
-  if constexpr (E == 2 && grp_pbytes(NP) >= 256 && MXA_GRP_ELEM_X) {
-    // a 32-position window (nsw <= 15): the swapping stops publish their ELEMENTS (right
-    // stop of top rank t at slot t, left stop of rank t at slot 16 + t -- 256 B of P, which
-    // NP >= 256 rows have), and
-    // each reads its partner's straight into its own position: one round trip fewer than
-    // publishing positions.  Position m holds old f since the median swap.
-    lu64* xs = (lu64*)(lu32*)g.P;
-    uint64_t el[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) el[e] = lb + e == m ? xf : (((uint64_t)K[e] << 32) | I2[e]);
-    int tg[2], sw[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int sh = 1 - e;
-      const int tl = (int)(PL + (uint32_t)__popc((Lm >> sh) >> 1));
-      const int tr = (int)(totR - PR - (uint32_t)__popc(Rm >> sh));
-      const bool isl = (SLm >> sh) & 1u, isr = ((Rm >> sh) & 1u) && (uint32_t)tr < nsw;
-      sw[e] = isl ? 1 : (isr ? 2 : 0);
-      tg[e] = isl ? tl : tr;
-      if (sw[e]) xs[(sw[e] == 1 ? 16 : 0) + tg[e]] = el[e];
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-      if (sw[e]) g.A[lb + e] = xs[(sw[e] == 1 ? 0 : 16) + tg[e]];
-    wave_lds_sync();
-    return cut;
-  }
   const uint32_t ob = NP <= 256 ? (uint32_t)(size_t)g.P : 0u;
   const uint32_t trash = ob + 2 * HP + gl, lbase = ob + HP + PL, rbase = ob + totR - PR, rlim = ob + nsw;
 #pragma unroll
@@ -281,7 +290,7 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
   for (uint32_t t = gl; __builtin_amdgcn_ballot_w64(t < nsw) != 0; t += 16) {
     if (t < nsw) {
       const uint32_t y = p_get<NP>(g, t), x = p_get<NP>(g, HP + t);
-      const uint64_t ax = g.A[x], ay = g.A[y];
+      const El ax = g.A[x], ay = g.A[y];
       g.A[x] = ay;
       g.A[y] = ax;
     }
@@ -295,81 +304,111 @@ __device__ __forceinline__ int grp_partition(const GrpRow& g, int f, int l, int 
 // The base is min(f & ~1, NPA - 16 E); a range fits iff need = l - (f & ~1) <= 16 E
 // (when the base is clamped, l <= NPA makes it fit anyway), so each candidate width
 // costs one compare of the precomputed need.
-template <int E, int NP>
-__device__ __forceinline__ bool grp_try(const GrpRow& g, int f, int l, int need, bool act, int gl, int& cut) {
+template <int E, int NP, typename El>
+__device__ __forceinline__ bool grp_try(const GrpRow<El>& g, int f, int l, int need, bool act, int gl, int& cut) {
   if (16 * E > NP || 16 * E > g.npa) return false;
   if (__builtin_amdgcn_ballot_w64(need > 16 * E) != 0) return false;
-  cut = grp_partition<E, NP>(g, f, l, min(f & ~1, g.npa - 16 * E), act, gl);
+  cut = grp_partition<E, NP, El>(g, f, l, min(f & ~1, g.npa - 16 * E), act, gl);
   return true;
 }
-template <int NP>
-__device__ __forceinline__ int grp_partition_any(const GrpRow& g, int f, int l, bool act, int gl) {
+template <int NP, typename El>
+__device__ __forceinline__ int grp_partition_any(const GrpRow<El>& g, int f, int l, bool act, int gl) {
   int cut = 0;
   const int need = act ? l - (f & ~1) : 0;
-  if (grp_try<2, NP>(g, f, l, need, act, gl, cut) || grp_try<4, NP>(g, f, l, need, act, gl, cut) ||
-      grp_try<6, NP>(g, f, l, need, act, gl, cut) || grp_try<8, NP>(g, f, l, need, act, gl, cut) ||
-      grp_try<10, NP>(g, f, l, need, act, gl, cut) || grp_try<12, NP>(g, f, l, need, act, gl, cut) ||
-      grp_try<14, NP>(g, f, l, need, act, gl, cut) || grp_try<16, NP>(g, f, l, need, act, gl, cut) ||
-      grp_try<24, NP>(g, f, l, need, act, gl, cut))
+  if (grp_try<2, NP, El>(g, f, l, need, act, gl, cut) || grp_try<4, NP, El>(g, f, l, need, act, gl, cut) ||
+      grp_try<6, NP, El>(g, f, l, need, act, gl, cut) || grp_try<8, NP, El>(g, f, l, need, act, gl, cut) ||
+      grp_try<10, NP, El>(g, f, l, need, act, gl, cut) || grp_try<12, NP, El>(g, f, l, need, act, gl, cut) ||
+      grp_try<14, NP, El>(g, f, l, need, act, gl, cut) || grp_try<16, NP, El>(g, f, l, need, act, gl, cut) ||
+      grp_try<24, NP, El>(g, f, l, need, act, gl, cut))
     return cut;
-  if constexpr (NP >= 512) cut = grp_partition<32, NP>(g, f, l, min(f & ~1, g.npa - 512), act, gl);
+  if constexpr (NP >= 512) cut = grp_partition<32, NP, El>(g, f, l, min(f & ~1, g.npa - 512), act, gl);
   return cut;
 }
 
 // stable rank of [0, m) (m <= 16 EP): lane gl holds positions EP gl + e; a position's
 // rank counts the keys greater than its own and the equal keys before it
-template <int EP>
-__device__ __forceinline__ void grp_rank_prefix(const GrpRow& g, int m, bool valid, int gl) {
+template <int EP, typename El>
+__device__ __forceinline__ void grp_rank_prefix(const GrpRow<El>& g, int m, bool valid, int gl) {
   const int z0 = EP * gl;
-  uint32_t K[EP], I[EP], r[EP];
+  uint32_t r[EP];
+  if constexpr (sizeof(El) == 8) {
+    uint32_t K[EP], I[EP];
 #pragma unroll
-  for (int e = 0; e < EP; e += 2) {
-    const u32x4 v = *(const lu128*)(g.A + z0 + e);
-    I[e] = v.x;
-    K[e] = v.y;
-    I[e + 1] = v.z;
-    K[e + 1] = v.w;
-    r[e] = r[e + 1] = 0u;
+    for (int e = 0; e < EP; e += 2) {
+      const u32x4 v = *(const lu128*)(g.A + z0 + e);
+      I[e] = v.x;
+      K[e] = v.y;
+      I[e + 1] = v.z;
+      K[e + 1] = v.w;
+      r[e] = r[e + 1] = 0u;
+    }
+    // composites (key << 32 | 0xFFFF - position): unique, larger for the earlier of two
+    // equal keys, so a position's rank is the number of larger composites
+    uint64_t C[EP];
+#pragma unroll
+    for (int e = 0; e < EP; ++e) C[e] = ((uint64_t)K[e] << 32) | (uint32_t)(0xFFFF - (z0 + e));
+    for (int w = 0; w < m; ++w) {
+      const uint64_t cw = (g.A[w] & 0xFFFFFFFF00000000ull) | (uint32_t)(0xFFFF - w);
+#pragma unroll
+      for (int e = 0; e < EP; ++e) r[e] = g_add_gt(r[e], cw, C[e]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < EP; ++e)
+      if (valid && z0 + e < m) g.A[r[e]] = pack_ki(K[e], I[e]);
+  } else {
+    // packed: composites (element & ~0xFF) | 255 - position (m <= 64)
+    uint32_t X[EP], C[EP];
+#pragma unroll
+    for (int e = 0; e < EP; e += 2) {
+      const uint64_t v = *(const __attribute__((address_space(3))) uint64_t*)(g.A + z0 + e);
+      X[e] = (uint32_t)v;
+      X[e + 1] = (uint32_t)(v >> 32);
+      r[e] = r[e + 1] = 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < EP; ++e) C[e] = (X[e] & ~0xFFu) | (uint32_t)(255 - (z0 + e));
+    for (int w = 0; w < m; ++w) {
+      const uint32_t cw = (g.A[w] & ~0xFFu) | (uint32_t)(255 - w);
+#pragma unroll
+      for (int e = 0; e < EP; ++e) r[e] = g_add_gt32(r[e], cw, C[e]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < EP; ++e)
+      if (valid && z0 + e < m) g.A[r[e]] = X[e];
   }
-  // composites (key << 32 | 0xFFFF - position): unique, larger for the earlier of two
-  // equal keys, so a position's rank is the number of larger composites
-  uint64_t C[EP];
-#pragma unroll
-  for (int e = 0; e < EP; ++e) C[e] = ((uint64_t)K[e] << 32) | (uint32_t)(0xFFFF - (z0 + e));
-  for (int w = 0; w < m; ++w) {
-    const uint64_t cw = (g.A[w] & 0xFFFFFFFF00000000ull) | (uint32_t)(0xFFFF - w);
-#pragma unroll
-    for (int e = 0; e < EP; ++e) r[e] = g_add_gt(r[e], cw, C[e]);
-  }
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < EP; ++e)
-    if (valid && z0 + e < m) g.A[r[e]] = pack_ki(K[e], I[e]);
 }
 
 // stable rank of each queued segment (2..16 elements), one lane per segment: the rank
 // of element i counts the later elements with a larger key and the earlier ones with a
 // larger or equal key -- r[i] starts at i and each pair (i < j) moves one count with
 // one 32-bit compare (few registers live: the elements are re-read for the moves)
-__device__ __forceinline__ void grp_rank_segments(const GrpRow& g, int ns, int gl) {
+template <typename El>
+__device__ __forceinline__ void grp_rank_segments(const GrpRow<El>& g, int ns, int gl) {
   if (gl < ns) {
     const uint32_t sg = g.seg[gl];
     const int f = (int)(sg & 0xFFFFu), len = (int)(sg >> 16) - f;
-    const lu32* A32 = (const lu32*)g.A;
-    uint32_t kk[16], r[16];
+    uint32_t kk[16], kr[16], r[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      kk[i] = i < len ? A32[2 * (f + i) + 1] : 0u;  // key 0 sorts after every real key
+      if constexpr (sizeof(El) == 8) {
+        kk[i] = i < len ? ((const lu32*)g.A)[2 * (f + i) + 1] : 0u;  // key 0 sorts after every real key
+        kr[i] = kk[i];
+      } else {
+        kk[i] = i < len ? (uint32_t)g.A[f + i] : 0u;  // packed: key(j) > key(i) <=> x_j > (x_i | 0xFF)
+        kr[i] = kk[i] | 0xFFu;
+      }
       r[i] = (uint32_t)i;
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
 #pragma unroll
-      for (int j = i + 1; j < 16; ++j) g_pair_rank(r[i], r[j], kk[j], kk[i]);
+      for (int j = i + 1; j < 16; ++j) g_pair_rank(r[i], r[j], kk[j], kr[i]);
     }
-    uint64_t x[16];
+    El x[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = i < len ? (uint64_t)g.A[f + i] : 0ull;
+    for (int i = 0; i < 16; ++i) x[i] = i < len ? (El)g.A[f + i] : (El)0;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i < len) g.A[f + r[i]] = x[i];
@@ -381,10 +420,13 @@ __device__ __forceinline__ void grp_rank_segments(const GrpRow& g, int ns, int g
 // (or std::partial_sort when k*64 <= n) on every row of the wave.  One loop drives
 // both: each trip, every row settles its bookkeeping (exec-divergent, cheap) and then
 // every row with a pending range takes part in ONE partition step, so rows still in
-// the selection and rows already sorting share the wave's steps.  Afterwards g.A[p],
-// p < k, holds torch's p-th index in its low word.
-template <int NP>
-__device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool valid, int gl) {
+// the selection and rows already sorting share the wave's steps.  Afterwards
+// GEl<El>::idx(g.A[p]), p < k, is torch's p-th index.
+// QM: 0 = the final sort decided at run time, 1 = k - 1 <= 64 (the whole prefix ranked
+// at once), 2 = k - 1 > 64 (final segments queued and ranked one lane each) -- the fixed
+// forms leave the other ranking code (and its registers) out of the kernel.
+template <int NP, typename El = uint64_t, int QM = 0>
+__device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool valid, int gl) {
   if (k <= 0) return;
   if (k * 64 <= n) {  // std::partial_sort(begin, begin + k, end)
     if (valid && gl == 0) {
@@ -395,7 +437,7 @@ __device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool val
     return;
   }
   const int nth = k - 1, m = k - 1;
-  const bool queue = m > 64;  // final sort segments ranked one lane each (else the whole prefix)
+  const bool queue = QM == 0 ? m > 64 : QM == 2;  // final sort segments ranked one lane each (else the whole prefix)
   int ph = valid ? 0 : 2;     // 0 __introselect, 1 __introsort_loop, 2 done
   int f = 0, l = n, d = 2 * ilog2(n), sp = 0, ns = 0;
   while (true) {
@@ -403,7 +445,7 @@ __device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool val
       if (l - f > 3) {  // depth limit: __heap_select(f, nth + 1, l); iter_swap(f, nth)
         if (gl == 0) {
           ln_heap_select(g.A, f, nth + 1, l);
-          const uint64_t t = g.A[f];
+          const El t = g.A[f];
           g.A[f] = g.A[nth];
           g.A[nth] = t;
         }
@@ -423,7 +465,7 @@ __device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool val
             ln_heap_select(g.A, f, l, l);
             ln_sort_heap(g.A, f, l);
           }
-        } else if (queue && l - f >= 2) {
+        } else if (QM != 1 && queue && l - f >= 2) {
           g.seg[ns] = (uint32_t)f | ((uint32_t)l << 16);
           ++ns;
           if (ns == kGSeg) {
@@ -460,9 +502,9 @@ __device__ __forceinline__ void grp_topk(const GrpRow& g, int n, int k, bool val
     }
   }
   wave_lds_sync();
-  if (queue) {
+  if (QM != 1 && queue) {
     if (valid && ns > 0) grp_rank_segments(g, ns, gl);
-  } else if (m >= 2) {
+  } else if (QM != 2 && m >= 2) {
     if (m <= 32) grp_rank_prefix<2>(g, m, valid, gl);
     else grp_rank_prefix<4>(g, m, valid, gl);
   }

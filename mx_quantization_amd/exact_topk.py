@@ -15,8 +15,9 @@ the given modules to `TORCH`: a namespace that forwards every attribute to torch
     M.bind_exact_topk(models)          # its `torch.topk(...)` calls now give CPU order
 
 Covered: device tensors of float32 / float16 / bfloat16, the last dim, largest=True,
-sorted=True (the only form the modules use), up to 512 columns (longer rows raise
-NativeError, include/mxa.h MXA_ERR_UNSUPPORTED).  Other forms (largest=False,
+sorted=True (the only form the modules use), up to 1,024 columns (include/mxa.h
+kWMaxN: the PixArt 512x512 self-attention rows; longer rows raise NativeError,
+MXA_ERR_UNSUPPORTED).  Other forms (largest=False,
 sorted=False, another dim, CPU tensors) are torch's own topk, unchanged.
 """
 from __future__ import annotations

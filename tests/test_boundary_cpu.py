@@ -251,3 +251,73 @@ def test_committed_profiles_name_current_kernels():
         with open(os.path.join(ROOT, "profiles", f"{bench.PROFILE_TAG}_traffic_{cfg}.json")) as fh:
             sel = [k for k in json.load(fh)["kernels"] if bench.stage_of_kernel(k) == "select"]
         assert len(sel) == 1 and sel[0] in kernels, sel
+
+
+def _header_params():
+    """{function: [parameter declarations]} of every extern entry point in include/mxa.h."""
+    import re
+    src = open(os.path.join(ROOT, "include", "mxa.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for m in re.finditer(r"\b(?:int|int64_t|int32_t|const char\*|void)\s+\**(mxa_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(1)] = args
+    return out
+
+
+def _ctype_of_decl(decl):
+    """The ctypes type a C parameter declaration binds to (pointers -> c_void_p)."""
+    import ctypes
+    d = decl.replace("const ", "").strip()
+    if "*" in d or d.startswith("hipStream_t"):
+        return ctypes.c_void_p
+    base = d.split()[0]
+    return {"int64_t": ctypes.c_int64, "int32_t": ctypes.c_int32, "int": ctypes.c_int32, "float": ctypes.c_float,
+            "uint32_t": ctypes.c_uint32}[base]
+
+
+def test_integration_stubs_match_abi():
+    """Every reference-side ctypes stub in INTEGRATION.md (`_lib.<fn>.argtypes = [...]`)
+    has the argument count and order of include/mxa.h and of _native._SIGS, and every
+    call of such a stub in the document passes that many arguments."""
+    import ast
+    import ctypes
+    import re
+    from mx_quantization_amd import _native
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    hdr = _header_params()
+    stubs = re.findall(r"_lib\.(mxa_\w+)\.argtypes\s*=\s*(\[[^\]]*\])", doc)
+    assert stubs, "no ctypes stubs found in INTEGRATION.md"
+    alias = {"ctypes.c_void_p": ctypes.c_void_p, "ctypes.c_int64": ctypes.c_int64, "ctypes.c_int32": ctypes.c_int32,
+             "ctypes.c_float": ctypes.c_float, "ctypes.c_uint32": ctypes.c_uint32}
+    for fn, lst in stubs:
+        names = [t.strip() for t in lst.strip("[]").split(",") if t.strip()]
+        types = [alias[n] for n in names]
+        assert fn in hdr, f"{fn}: not declared in include/mxa.h"
+        want = [_ctype_of_decl(d) for d in hdr[fn]]
+        assert types == want, f"{fn}: INTEGRATION.md stub {names} != include/mxa.h {hdr[fn]}"
+        sig = _native._SIGS[fn][1]
+        assert [t for t in sig] == want, f"{fn}: _native._SIGS disagrees with include/mxa.h"
+        # every call of the stub in the document passes len(want) arguments
+        for call in re.finditer(r"_lib\." + fn + r"\(", doc):
+            i, depth = call.end(), 1
+            while depth:
+                depth += {"(": 1, ")": -1}.get(doc[i], 0)
+                i += 1
+            node = ast.parse("f(" + doc[call.end():i], mode="eval").body
+            assert len(node.args) == len(want), f"{fn}: a call in INTEGRATION.md passes {len(node.args)} arguments"
+
+
+def test_native_sigs_match_header():
+    """_native._SIGS binds every include/mxa.h entry point with its parameter types."""
+    from mx_quantization_amd import _native
+    hdr = _header_params()
+    import ctypes
+
+    def norm(t):  # a typed pointer binds like c_void_p
+        return ctypes.c_void_p if isinstance(t, type) and issubclass(t, ctypes._Pointer) else t
+
+    for fn, params in hdr.items():
+        assert fn in _native._SIGS, f"{fn} not bound in _native._SIGS"
+        assert [norm(t) for t in _native._SIGS[fn][1]] == [_ctype_of_decl(d) for d in params], fn

@@ -69,6 +69,7 @@ def test_bench_main_two_ranks_gathers_and_checks_every_shard(scaling):
                       "--parity-images", "2"])
     assert res["n_gpus"] == 2 and res["scaling"] == scaling
     assert res["config"]["parallelism"] == "dp2"
+    assert res["dist"] == {"initialized": True, "world_size": 2, "backend": "gloo"}
     # the MAX over ranks: at least the slower rank's region (0.1 s)
     assert res["ms_per_step"] * res["steps"] >= 100.0
     par = res["parity"]
@@ -120,7 +121,8 @@ def test_bench_byte_and_op_accounting():
 
 def test_hbm_traffic_kernel_names_map_to_bench_stages():
     ht = _load_hbm_traffic()
-    assert ht.stage_of("void mxa::select_kernel<256, 3>(mxa::Rows2Args)") == "select"
+    assert ht.stage_of("void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)") == "select"
+    assert ht.stage_of("void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)") == "select_fb"
     assert ht.stage_of("void mxa::finish_kernel<2, 2>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("void mxa::dense_rows_kernel<4>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("mxa::attn_prep_kernel(mxa::RowsPrepArgs, mxa::RowsPrepArgs, mxa::ColsPrepArgs, unsigned int, "
@@ -141,7 +143,8 @@ def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
     DiT's select_kernel<256,3,4> dispatches: per-instantiation keys keep them apart, and a
     stage with two instantiations in one run gets no traffic number at all."""
     ht = _load_hbm_traffic()
-    deit, dit = "void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)", "void mxa::select_kernel<256, 3, 4>(mxa::Rows2Args)"
+    deit, dit = ("void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)",
+                 "void mxa::select_q_kernel<256, 3, 4, 16, true>(mxa::Rows2Args)")
     fin = "void mxa::finish_kernel<2, 12, true>(mxa::Rows2Args)"
     rows = []
     for name, kib_f, kib_w, n in ((deit, 10.0, 143250.0, 7), (dit, 20.0, 473145.0, 3), (fin, 100.0, 200.0, 7)):
@@ -161,7 +164,7 @@ def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
 
 def test_bench_limiter_from_profiles(tmp_path):
     import bench
-    sel = "void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)"
+    sel = "void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)"
     tj, pj = tmp_path / "t.json", tmp_path / "p.json"
     tj.write_text(json.dumps({"stages": {"select": 160e6}}))
     # 0.5 ms: HBM 160 MB -> 0.04 of peak; VALU 436 M instr x 2 cycles over 1024 SIMDs at 2.4 GHz -> 0.71
@@ -172,7 +175,7 @@ def test_bench_limiter_from_profiles(tmp_path):
     assert abs(lim["fracs"]["valu_issue"] - 436e6 * 2 / (1024 * 2.4e9 * 0.5e-3)) < 1e-9
     assert lim["lds_conflict_cycles_per_lds_instr"] == 0.5
     # two instantiations of the stage in the PMC file: no kernel is picked
-    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("2>", "4>"): {"SQ_INSTS_VALU": 1.0}}))
+    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("false>", "true>"): {"SQ_INSTS_VALU": 1.0}}))
     _, lim = bench.profile_of({"pmc": str(pj)}, "select", 0.5, 320.0)
     assert "kernel" not in lim and lim["bound"] == "hbm"
 

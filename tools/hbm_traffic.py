@@ -25,8 +25,10 @@ import sys
 
 
 def stage_of(kernel):
-    if "select_kernel" in kernel or "select_wave_kernel" in kernel:
+    if "select_q_kernel" in kernel:  # the packed-element selection kernel
         return "select"
+    if "select_kernel" in kernel:  # the 64-bit one: rows the packed kernel leaves, true scores, ELSA
+        return "select_fb"
     if "finish_kernel" in kernel or "finish16_kernel" in kernel or "dense_rows_kernel" in kernel:
         return "finish"
     if "attn_prep_kernel" in kernel:
