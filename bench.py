@@ -86,8 +86,8 @@ def stage_bytes(c, path):
     vtab = D * tpad + 2 * ntb * D
     by = {"prep": h * (4 * N * D + codes(N) + apx(N)) + h * (4 * T * D + codes(T) + apx(T)) + h * (4 * T * D + vtab)}
     if path == "rows_split":
-        by["select"] = h * (apx(N) + apx(T) + 8 * N * k + 4 * N * k)
-        by["finish"] = h * (codes(N) + codes(T) + vtab + 4 * N * k + 4 * N * D)
+        by["select"] = h * (apx(N) + apx(T) + 8 * N * k)  # the int64 idx, which the finishing kernel reads
+        by["finish"] = h * (codes(N) + codes(T) + vtab + 8 * N * k + 4 * N * D)
     else:  # dense: stage 3 empty, stage 4 the row kernel
         by["select"] = 0
         by["finish"] = h * (codes(N) + codes(T) + vtab + 4 * N * D)

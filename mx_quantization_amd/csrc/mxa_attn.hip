@@ -70,7 +70,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 // workspace regions, 256-B aligned
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx32;
+  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail;
   int64_t xc, xs, slow;  // fused qkv projection: x codes / exponents, slow-head list
   int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
                               // copy (D % 32 != 0 only), the GEMM's fp64 wave list
@@ -128,7 +128,11 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
   L.knorm = take(mode == kModeElsa ? krows * 4 : 0);
   L.vt = take(BH * p->D * (int64_t)L.tpad);
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
-  L.idx32 = take(p->top_k ? qrows * (int64_t)p->k_top * 4 : 0);
+  L.idx16 = take(p->top_k ? qrows * (int64_t)p->k_top * 2 : 0);  // used when the caller takes no idx
+  {  // the one-lane top-k tail's staging records (mxa_tail.hpp)
+    const int tw = p->top_k ? sel_tail_width(mode, p->T, p->k_top) : 0;
+    L.tail = take(tw ? qrows * (int64_t)tail_rec_words(tw) * 4 : 0);
+  }
   if (xq) {
     const int64_t nbk = (xq->C + 31) / 32, tokens = (int64_t)p->B * p->N;
     L.xc = take(tokens * nbk * 32);
@@ -383,7 +387,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.bs0 = pp.bias_strides[0]; r2.bs1 = pp.bias_strides[1]; r2.bs2 = pp.bias_strides[2]; r2.bs3 = pp.bias_strides[3];
   r2.out = pp.out; r2.os0 = pp.out_strides[0]; r2.os1 = pp.out_strides[1]; r2.os2 = pp.out_strides[2];
   r2.idx_out = pp.idx_out; r2.true_out = pp.true_out; r2.pred_out = pp.pred_out; r2.mask_out = pp.mask_out;
-  r2.idx32 = reinterpret_cast<int32_t*>(ws + L.idx32);
+  r2.idx16 = reinterpret_cast<uint16_t*>(ws + L.idx16);
+  r2.tail_rec = reinterpret_cast<uint32_t*>(ws + L.tail);
   const bool direct = pj && proj_codes_direct(&pp);
   if (direct) {  // the finishing kernel writes the proj's input codes
     r2.xo_codes = reinterpret_cast<int8_t*>(ws + L.yc);

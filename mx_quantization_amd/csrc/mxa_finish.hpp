@@ -146,7 +146,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
   #pragma unroll
       for (int t = 0; t < KS; ++t) {
         const int s = gl + 16 * t;
-        in.ix[t] = valid && s < k ? a.idx32[grow * k + s] : -1;
+        in.ix[t] = valid && s < k ? kept_get(a, grow * k + s) : -1;
       }
     };
     PassIn nxt;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(512) void finish_kernel(Rows2Args a) {
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
       const int sl = ph + 2 * t;
-      in.ix[t] = valid && sl < k ? a.idx32[grow * k + sl] : -1;
+      in.ix[t] = valid && sl < k ? kept_get(a, grow * k + sl) : -1;
     }
   };
   TileIn tnxt;

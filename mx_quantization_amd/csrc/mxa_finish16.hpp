@@ -128,7 +128,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
       const int s = ph + LPR * t;
-      in.ix[t] = valid && s < k ? a.idx32[grow * k + s] : -1;
+      in.ix[t] = valid && s < k ? kept_get(a, grow * k + s) : -1;
     }
   };
 

@@ -10,6 +10,21 @@ inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr
 
 // selection kernel (mxa_sel.hip); plan: only check the LDS budget, launch nothing
 int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);
+#ifndef MXA_TAIL_PREF
+#define MXA_TAIL_PREF 64  // the one-lane tail's prefix when k allows (32 or 64)
+#endif
+// the selection's packed pass (rows of <= 256 keys, the approximators whose scores pack)
+inline bool sel_packs(int mode, int T) {
+  return T <= 256 && (mode == kModeExSign || mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx);
+}
+// the prefix the one-lane tail takes over (mxa_tail.hpp), 0 = none: k + 2 <= TW (the
+// introselect's last range and the sort of [0, k-1) lie in it), not partial_sort (k*64 <= T)
+inline int sel_tail_width(int mode, int T, int k) {
+  if (!sel_packs(mode, T) || k <= 0 || (int64_t)k * 64 <= T) return 0;
+  if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
+  return k + 2 <= 64 ? 64 : 0;
+}
+
 // one score mode per translation unit of mxa_sel.hip (MXA_SEL_PART 1..6)
 int launch_select_p1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // ex_pred
 int launch_select_p2(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // EXION

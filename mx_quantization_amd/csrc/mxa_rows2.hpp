@@ -44,14 +44,32 @@ struct Rows2Args {
   uint32_t* mask_out;
   int waves;        // waves per workgroup
   int rows_per_wg;  // query rows per workgroup (grid.y splits a head when there are few heads)
-  int32_t* idx32;  // split path: the kept indices [B*H*N][k_top] between the two kernels
-  int fb_only;     // selection kernel: only the rows the packed-element kernel left (idx32[row][0] < 0)
+  uint16_t* idx16;  // split path: the kept indices [B*H*N][k_top] between the two kernels when
+                    // the caller takes no idx_out (else the finishing kernel reads idx_out)
+  int fb_only;      // selection kernel: only the rows the packed pass left (kept_get(row * k) < 0)
+  uint32_t* tail_rec;  // the one-lane tail's staging records (mxa_tail.hpp), when it runs
   // finishing kernel with the proj Linear behind it (D % 32 == 0): the output rows
   // (B, N, H*D) MX-quantized along C straight from the P.V tile -- rows_prep's layout,
   // codes [B*N][H*D], code-unit exponents [B*N][H*D/32] -- instead of fp32 in `out`
   int8_t* xo_codes;
   int16_t* xo_exps;
 };
+
+// words of a one-lane top-k tail staging record (mxa_tail.hpp): state, pad, TW elements
+__host__ __device__ constexpr int tail_rec_words(int TW) { return TW + 4; }
+
+// the kept indices between the selection and the finishing kernel: the caller's int64
+// idx_out when it takes one (no second copy), else a 16-bit copy in the workspace; -1
+// (0xFFFF) marks a row the packed selection pass left for the 64-bit one
+__device__ __forceinline__ int kept_get(const Rows2Args& a, int64_t i) {
+  if (a.idx_out) return (int)a.idx_out[i];
+  const uint32_t v = a.idx16[i];
+  return v == 0xFFFFu ? -1 : (int)v;
+}
+__device__ __forceinline__ void kept_put(const Rows2Args& a, int64_t i, int ix) {
+  if (a.idx_out) a.idx_out[i] = (int64_t)ix;
+  else a.idx16[i] = (uint16_t)ix;
+}
 
 
 struct Rows2Lds {

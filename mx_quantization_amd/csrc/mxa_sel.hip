@@ -10,13 +10,13 @@ template <int NP, int MODE, int W, typename El>
 static size_t select_lds(const Rows2Args& ra) {
   return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP, sizeof(El));
 }
-template <int NP, int MODE, int W, typename El = uint64_t, int QM = 0>
+template <int NP, int MODE, int W, typename El = uint64_t, int QM = 0, int TW = 0>
 static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
   Rows2Args ra = ra0;
   const size_t lds = select_lds<NP, MODE, W, El>(ra);
   if (lds > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   if (plan) return MXA_OK;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W, El, QM>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W, El, QM, TW>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
@@ -24,24 +24,49 @@ static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, boo
   while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
   ra.rows_per_wg = rows;
   const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
+  hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM, TW>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+// the one-lane tail (mxa_tail.hpp) over every row of the call: the rows the packed pass
+// handed over
+template <int TW>
+static int launch_tail(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (plan) return MXA_OK;
+  TailArgs ta{ra.tail_rec, (int64_t)BH * ra.N, ra.k_top, (ra.T + 31) / 32, ra.idx_out, ra.idx16, ra.mask_out};
+  const size_t lds = tail_lds(TW);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tail_kernel<TW>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  const int64_t per = 64 * kTailWaves;
+  hipLaunchKernelGGL(topk_tail_kernel<TW>, dim3((unsigned)((ta.rows + per - 1) / per)), dim3(64 * kTailWaves), lds, stream, ta);
+  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+template <int NP, int MODE, int W>
+static int launch_select_packed(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  const int tw = sel_tail_width(MODE, ra.T, ra.k_top);
+  int rc;
+  if (tw == 32) {
+    rc = launch_select_w<NP, MODE, W, uint32_t, 1, 32>(ra, BH, stream, plan);
+    if (rc == MXA_OK) rc = launch_tail<32>(ra, BH, stream, plan);
+  } else if (tw == 64) {
+    rc = launch_select_w<NP, MODE, W, uint32_t, 1, 64>(ra, BH, stream, plan);
+    if (rc == MXA_OK) rc = launch_tail<64>(ra, BH, stream, plan);
+  } else {
+    rc = launch_select_w<NP, MODE, W, uint32_t, 0, 0>(ra, BH, stream, plan);
+  }
+  return rc;
 }
 template <int NP, int MODE>
 static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
   const int wsel = sel_waves_for(ra.T, BH, ra.N);
   // packed elements (rows of <= 256 keys) for the approximators whose scores are sums of
-  // small integers times powers of two; then the 64-bit kernel on the rows whose scores do
-  // not pack (fb_only: its workgroups without such rows return at once).  The true scores,
-  // ELSA and longer rows: the 64-bit kernel alone.
-  constexpr bool kPack = MODE == kModeExSign || MODE == kModeOpExp || MODE == kModeOpMul || MODE == kModeTrueEx;
-  if constexpr (kPack && NP <= 256) {
-    if (ra.k_top > 0) {
-      const bool q = ra.k_top - 1 > 64;
-      const int rc = wsel == 2 ? (q ? launch_select_w<NP, MODE, 2, uint32_t, 2>(ra, BH, stream, plan)
-                                    : launch_select_w<NP, MODE, 2, uint32_t, 1>(ra, BH, stream, plan))
-                               : (q ? launch_select_w<NP, MODE, 4, uint32_t, 2>(ra, BH, stream, plan)
-                                    : launch_select_w<NP, MODE, 4, uint32_t, 1>(ra, BH, stream, plan));
+  // small integers times powers of two (the one-lane tail behind it for small k); then the
+  // 64-bit kernel on the rows whose scores do not pack (fb_only: its workgroups without
+  // such rows return at once).  The true scores, ELSA and longer rows: the 64-bit kernel.
+  if constexpr (NP <= 256) {
+    if (sel_packs(MODE, ra.T) && ra.k_top > 0) {
+      const int rc = wsel == 2 ? launch_select_packed<NP, MODE, 2>(ra, BH, stream, plan)
+                               : launch_select_packed<NP, MODE, 4>(ra, BH, stream, plan);
       if (rc != MXA_OK) return rc;
       Rows2Args fb = ra;
       fb.fb_only = 1;

@@ -9,8 +9,9 @@
 //   approx off     MXINT8 codes + exponents (the true scores are ranked)
 // then per row (sel_scores): the scores (exact fp64 block epilogue where needed: the
 // scores are exact sums of integer * 2^e), bias added in fp32 as the caller
-// does; torch's CPU topk index order; the k kept indices as int64 (the op's idx) and int32
-// (the finishing kernel's input), and the prune-mask words when asked for.
+// does; torch's CPU topk index order; the k kept indices (the op's int64 idx, which the
+// finishing kernel reads too, or a 16-bit workspace copy: kept_put), and the prune-mask
+// words when asked for.
 //   select_kernel<..., uint32_t>  rows of <= 256 keys whose scores pack into 32-bit
 //                     elements (mxa_topk_grp.hpp GEl), then
 //   select_kernel<..., uint64_t>  the rows that do not (fb_only), and every row of the true
@@ -23,6 +24,7 @@
 #include <type_traits>
 #include "mxa_rows2.hpp"
 #include "mxa_topk_grp.hpp"
+#include "mxa_tail.hpp"
 #include "mxa_topk_wave.hpp"
 
 namespace mxa {
@@ -409,10 +411,14 @@ __device__ __forceinline__ void sel_mask_words(const Rows2Args& a, __attribute__
 
 // ---- four query rows per wave (mxa_topk_grp.hpp) ---------------------------------
 // rows rq + (lane >> 4) of head bh; g0 = the wave's per-row areas (grp_row_bytes each).
-// El = uint64_t: any row (a.fb_only: only the rows the packed pass left, idx32[row][0] < 0).
+// El = uint64_t: any row (a.fb_only: only the rows the packed pass left, kept_get(row * k) < 0).
 // El = uint32_t (packed): a row whose scores do not all leave the key's low byte free is
-// left for the 64-bit pass: idx32[row][0] = -1.
-template <int NP, int MODE, typename El, int QM>
+// left for the 64-bit pass: its first kept index is -1 (kept_put).
+// TW > 0 (packed): rows whose remaining work fits a TW-position prefix go to the one-lane
+// tail kernel (mxa_tail.hpp): their state and prefix are written to a.tail_rec (and the
+// first kept index set to 0, so the 64-bit pass leaves them alone); it writes their
+// indices and mask words.
+template <int NP, int MODE, typename El, int QM, int TW = 0>
 __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, unsigned char* g0, int bh, int rq,
                                           int r_end, int lane) {
   constexpr bool kPacked = sizeof(El) == 4;
@@ -423,7 +429,7 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
   const int r = rq + gi;
   bool valid = r < r_end;
   const int64_t grow = (int64_t)bh * a.N + (valid ? r : rq);
-  if (!kPacked && a.fb_only && valid) valid = a.idx32[grow * k] < 0;
+  if (!kPacked && a.fb_only && valid) valid = kept_get(a, grow * k) < 0;
   uint32_t bad = 0u;
 #ifdef MXA_SEL_SKIP
   if (valid && !((MXA_SEL_SKIP) & 2))
@@ -451,7 +457,7 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
   if constexpr (kPacked) {  // this row's 16 lanes: any score that does not pack
     const uint64_t bw = __builtin_amdgcn_ballot_w64(bad != 0u);
     if (valid && ((bw >> (16 * gi)) & 0xFFFFull) != 0) {
-      if (gl == 0) a.idx32[grow * k] = -1;
+      if (gl == 0) kept_put(a, grow * k, -1);
       valid = false;
     }
   }
@@ -459,13 +465,23 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
 #ifdef MXA_SEL_SKIP  // 1 = no top-k
   if (!((MXA_SEL_SKIP) & 1))
 #endif
-  grp_topk<NP, El, QM>(g, T, k, valid, gl);
+  GrpHand hand{0u, false};
+  grp_topk<NP, El, QM, TW>(g, T, k, valid, gl, &hand);
+  if (TW > 0 && hand.on) {  // the row's state and prefix to the tail kernel
+    uint32_t* rec = a.tail_rec + grow * tail_rec_words(TW);
+    if (gl == 0) {
+      rec[0] = hand.state | kTailPending;
+      kept_put(a, grow * k, 0);
+    }
+    for (int p = gl; p < TW; p += 16) rec[4 + p] = (uint32_t)g.A[p];
+    valid = false;
+  } else if (TW > 0 && r < r_end) {  // finished here, or left for the 64-bit pass: not the tail's
+    if (gl == 0) a.tail_rec[grow * tail_rec_words(TW)] = 0u;
+  }
   // kept indices: four consecutive rows per wave
   if (valid) {
     for (int p = gl; p < k; p += 16) {
-      const uint32_t ix = GEl<El>::idx(g.A[p]);
-      if (a.idx_out) a.idx_out[grow * k + p] = (int64_t)ix;
-      a.idx32[grow * k + p] = (int32_t)ix;
+      kept_put(a, grow * k + p, (int)GEl<El>::idx(g.A[p]));
     }
   }
   if (a.mask_out) sel_mask_words(a, g.stk, grow, valid, gl, 16, k, [&](int p) { return GEl<El>::idx(g.A[p]); });
@@ -476,7 +492,7 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
 // every approximator (a.fb_only: only the rows the packed pass left; a workgroup
 // without such rows returns at once).  El = uint32_t: the packed pass (rows of <= 256
 // keys; half the LDS per row, so more resident waves).
-template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0>
+template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
 __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? MXA_SELP_OCC : NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -485,7 +501,7 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
   if (sizeof(El) == 8 && a.fb_only) {
     int any = 0;
     for (int r = r0 + (int)threadIdx.x; r < r_end; r += blockDim.x)
-      any |= a.idx32[((int64_t)bh * a.N + r) * a.k_top] < 0;
+      any |= kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0;
     if (!__syncthreads_or(any)) return;
   }
   const SelLds L = sel_lds(MODE, a.T, a.D, a.kst, a.nbd);
@@ -494,10 +510,10 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
   for (int rq = r0 + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
     if (sizeof(El) == 8 && a.fb_only) {  // the rows of this group that are left
       const int r = min(rq + (lane >> 4), r_end - 1);
-      if (__builtin_amdgcn_ballot_w64(rq + (lane >> 4) < r_end && a.idx32[((int64_t)bh * a.N + r) * a.k_top] < 0) == 0)
+      if (__builtin_amdgcn_ballot_w64(rq + (lane >> 4) < r_end && kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0) == 0)
         continue;
     }
-    sel_rows4<NP, MODE, El, QM>(a, t, g0, bh, rq, r_end, lane);
+    sel_rows4<NP, MODE, El, QM, TW>(a, t, g0, bh, rq, r_end, lane);
   }
 }
 

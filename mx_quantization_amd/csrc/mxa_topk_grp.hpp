@@ -425,8 +425,17 @@ __device__ __forceinline__ void grp_rank_segments(const GrpRow<El>& g, int ns, i
 // QM: 0 = the final sort decided at run time, 1 = k - 1 <= 64 (the whole prefix ranked
 // at once), 2 = k - 1 > 64 (final segments queued and ranked one lane each) -- the fixed
 // forms leave the other ranking code (and its registers) out of the kernel.
-template <int NP, typename El = uint64_t, int QM = 0>
-__device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool valid, int gl) {
+// TW > 0 (packed rows, k + 2 <= TW): once a row's introselect range lies in [0, TW) --
+// or its selection ended at the depth limit -- the row is handed over to the one-lane
+// tail (mxa_tail.hpp) instead of finished here: *hand = its tail state (f | l << 8 |
+// d << 16 | phase << 24, phase 0 the introselect on [f, l), 1 the sort of [0, k-1)),
+// g.A[0, TW) its prefix; the sort phase and the final ranks never run here.
+struct GrpHand {
+  uint32_t state;
+  bool on;
+};
+template <int NP, typename El = uint64_t, int QM = 0, int TW = 0>
+__device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool valid, int gl, GrpHand* hand = nullptr) {
   if (k <= 0) return;
   if (k * 64 <= n) {  // std::partial_sort(begin, begin + k, end)
     if (valid && gl == 0) {
@@ -441,6 +450,11 @@ __device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool
   int ph = valid ? 0 : 2;     // 0 __introselect, 1 __introsort_loop, 2 done
   int f = 0, l = n, d = 2 * ilog2(n), sp = 0, ns = 0;
   while (true) {
+    if (TW > 0 && ph == 0 && l <= TW) {  // the rest fits the tail's prefix: hand it over
+      hand->state = (uint32_t)f | ((uint32_t)l << 8) | ((uint32_t)d << 16);
+      hand->on = true;
+      ph = 2;
+    }
     if (ph == 0 && (l - f <= 3 || d == 0)) {  // the selection ends
       if (l - f > 3) {  // depth limit: __heap_select(f, nth + 1, l); iter_swap(f, nth)
         if (gl == 0) {
@@ -456,6 +470,11 @@ __device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool
       f = 0;
       l = m;
       d = m > 1 ? 2 * ilog2(m) : 0;
+      if (TW > 0) {  // the sort of [0, k-1) to the tail
+        hand->state = 1u << 24;
+        hand->on = true;
+        ph = 2;
+      }
     }
     if (ph == 1) {
       // settle: finished segments (<= 16 elements, or heap-sorted at the depth limit)
@@ -502,13 +521,15 @@ __device__ __forceinline__ void grp_topk(const GrpRow<El>& g, int n, int k, bool
     }
   }
   wave_lds_sync();
-  if (QM != 1 && queue) {
-    if (valid && ns > 0) grp_rank_segments(g, ns, gl);
-  } else if (QM != 2 && m >= 2) {
-    if (m <= 32) grp_rank_prefix<2>(g, m, valid, gl);
-    else grp_rank_prefix<4>(g, m, valid, gl);
+  if constexpr (TW == 0) {
+    if (QM != 1 && queue) {
+      if (valid && ns > 0) grp_rank_segments(g, ns, gl);
+    } else if (QM != 2 && m >= 2) {
+      if (m <= 32) grp_rank_prefix<2>(g, m, valid, gl);
+      else grp_rank_prefix<4>(g, m, valid, gl);
+    }
+    wave_lds_sync();
   }
-  wave_lds_sync();
 }
 
 }  // namespace mxa

@@ -53,8 +53,9 @@ def test_workspace_formula():
     p.top_k, p.approx, p.k_top, p.pred_mode = 1, 1, 20, 0
     nbytes = N.lib().mxa_attention_workspace_bytes(ctypes.byref(p))
     # per head: Q,K codes + exponents + sign words (2 x 197 x (64 + 4 + 4 + 8) B),
-    # V^T codes + exponents (64 x 224 + 7 x 64 x 2 B), kept indices (197 x 20 x 4 B)
-    per_head = 2 * 197 * (64 + 4 + 4 + 8) + 64 * 224 + 7 * 64 * 2 + 197 * 20 * 4
+    # V^T codes + exponents (64 x 224 + 7 x 64 x 2 B), kept indices (197 x 20 x 2 B: the
+    # 16-bit copy for callers without idx)
+    per_head = 2 * 197 * (64 + 4 + 4 + 8) + 64 * 224 + 7 * 64 * 2 + 197 * 20 * 2
     assert 3072 * per_head <= nbytes < 3072 * per_head + 15 * 256
 
 

@@ -112,7 +112,7 @@ def test_bench_byte_and_op_accounting():
     dense = bench.stage_bytes(c, "rows_fused")
     h, N, k = c["B"] * c["H"], c["N"], c["k"]
     assert list(split) == list(dense) == list(bench.STAGES)
-    assert dense["select"] == 0 and split["finish"] - dense["finish"] == h * 4 * N * k
+    assert dense["select"] == 0 and split["finish"] - dense["finish"] == h * 8 * N * k
     assert bench.fused_min_bytes(c) == 716537856  # 716.5 MB at DeiT-base b256
     assert abs(bench.bytes_qa(c) - 633.2e6) < 0.1e6  # SURVEY.md §8d Bytes_qa
     assert abs(bench.ops_gemm(c) - 30.52e9) < 0.01e9  # SURVEY.md §8d Ops_gemm
