@@ -70,7 +70,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 // workspace regions, 256-B aligned
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail;
+  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail, fbf;
   int64_t xc, xs, slow;  // fused qkv projection: x codes / exponents, slow-head list
   int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
                               // copy (D % 32 != 0 only), the GEMM's fp64 wave list
@@ -129,9 +129,12 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
   L.vt = take(BH * p->D * (int64_t)L.tpad);
   L.vs = take(BH * L.ntb * (int64_t)p->D * 2);
   L.idx16 = take(p->top_k ? qrows * (int64_t)p->k_top * 2 : 0);  // used when the caller takes no idx
-  {  // the one-lane top-k tail's staging records (mxa_tail.hpp)
-    const int tw = p->top_k ? sel_tail_width(mode, p->T, p->k_top) : 0;
+  {  // the one-lane top-k tail's staging records (mxa_tail.hpp); the packed selection
+     // pass's per-workgroup flags (at most one workgroup per 16 query rows of a head)
+    const bool pk = p->top_k && sel_packs(mode, p->T, p->bias != nullptr);
+    const int tw = p->top_k ? sel_tail_width(mode, p->T, p->k_top, p->bias != nullptr) : 0;
     L.tail = take(tw ? qrows * (int64_t)tail_rec_words(tw) * 4 : 0);
+    L.fbf = take(pk ? BH * (int64_t)((p->N + 15) / 16) * 4 : 0);
   }
   if (xq) {
     const int64_t nbk = (xq->C + 31) / 32, tokens = (int64_t)p->B * p->N;
@@ -389,6 +392,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.idx_out = pp.idx_out; r2.true_out = pp.true_out; r2.pred_out = pp.pred_out; r2.mask_out = pp.mask_out;
   r2.idx16 = reinterpret_cast<uint16_t*>(ws + L.idx16);
   r2.tail_rec = reinterpret_cast<uint32_t*>(ws + L.tail);
+  r2.fb_flags = reinterpret_cast<uint32_t*>(ws + L.fbf);
   const bool direct = pj && proj_codes_direct(&pp);
   if (direct) {  // the finishing kernel writes the proj's input codes
     r2.xo_codes = reinterpret_cast<int8_t*>(ws + L.yc);

@@ -13,14 +13,17 @@ int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, boo
 #ifndef MXA_TAIL_PREF
 #define MXA_TAIL_PREF 64  // the one-lane tail's prefix when k allows (32 or 64)
 #endif
-// the selection's packed pass (rows of <= 256 keys, the approximators whose scores pack)
-inline bool sel_packs(int mode, int T) {
-  return T <= 256 && (mode == kModeExSign || mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx);
+// the selection's packed pass: rows of <= 256 keys, the approximators whose scores pack
+// (sums of a few small integers times powers of two), no bias (a bias of -10000 next to
+// small scores needs the key's low byte: PixArt's masked cross-attention would fall back
+// for every row)
+inline bool sel_packs(int mode, int T, bool bias) {
+  return !bias && T <= 256 && (mode == kModeExSign || mode == kModeOpExp || mode == kModeOpMul || mode == kModeTrueEx);
 }
 // the prefix the one-lane tail takes over (mxa_tail.hpp), 0 = none: k + 2 <= TW (the
 // introselect's last range and the sort of [0, k-1) lie in it), not partial_sort (k*64 <= T)
-inline int sel_tail_width(int mode, int T, int k) {
-  if (!sel_packs(mode, T) || k <= 0 || (int64_t)k * 64 <= T) return 0;
+inline int sel_tail_width(int mode, int T, int k, bool bias) {
+  if (!sel_packs(mode, T, bias) || k <= 0 || (int64_t)k * 64 <= T) return 0;
   if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
   return k + 2 <= 64 ? 64 : 0;
 }

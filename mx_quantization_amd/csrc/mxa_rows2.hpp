@@ -48,6 +48,8 @@ struct Rows2Args {
                     // the caller takes no idx_out (else the finishing kernel reads idx_out)
   int fb_only;      // selection kernel: only the rows the packed pass left (kept_get(row * k) < 0)
   uint32_t* tail_rec;  // the one-lane tail's staging records (mxa_tail.hpp), when it runs
+  uint32_t* fb_flags;  // packed selection pass: per workgroup (bh * gy + y), rows left for the 64-bit pass
+  int fb_gy;           // the packed pass's gy (fb_only launches)
   // finishing kernel with the proj Linear behind it (D % 32 == 0): the output rows
   // (B, N, H*D) MX-quantized along C straight from the P.V tile -- rows_prep's layout,
   // codes [B*N][H*D], code-unit exponents [B*N][H*D/32] -- instead of fp32 in `out`

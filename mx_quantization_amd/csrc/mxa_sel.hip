@@ -10,6 +10,13 @@ template <int NP, int MODE, int W, typename El>
 static size_t select_lds(const Rows2Args& ra) {
   return sel_lds(MODE, ra.T, ra.D, ra.kst, ra.nbd).rows + (size_t)4 * W * grp_row_bytes(grp_alloc(ra.T), NP, sizeof(El));
 }
+// query rows per selection workgroup: few heads (PixArt cross-attention) take shorter row
+// chunks so that the grid still fills the chip
+inline int sel_rows_per_wg(int BH, int N) {
+  int rows = kSelRows;
+  while (rows > 16 && (int64_t)BH * ((N + rows - 1) / rows) < 2048) rows -= 16;
+  return rows;
+}
 template <int NP, int MODE, int W, typename El = uint64_t, int QM = 0, int TW = 0>
 static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, bool plan) {
   Rows2Args ra = ra0;
@@ -19,12 +26,14 @@ static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, boo
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel<NP, MODE, W, El, QM, TW>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
-  // few heads (PixArt cross-attention): shorter row chunks so that the grid still fills the chip
-  int rows = kSelRows;
-  while (rows > 16 && (int64_t)BH * ((ra.N + rows - 1) / rows) < 2048) rows -= 16;
-  ra.rows_per_wg = rows;
-  const unsigned gy = (unsigned)((ra.N + rows - 1) / rows);
-  hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM, TW>), dim3((unsigned)BH, gy), dim3(64 * W), lds, stream, ra);
+  ra.rows_per_wg = sel_rows_per_wg(BH, ra.N);
+  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
+  dim3 grid((unsigned)BH, gy);
+  if (sizeof(El) == 8 && ra.fb_only) {  // one workgroup per 64 flags of the packed pass
+    ra.fb_gy = (int)gy;
+    grid = dim3((unsigned)(((int64_t)BH * gy + 63) / 64), 1);
+  }
+  hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM, TW>), grid, dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 // the one-lane tail (mxa_tail.hpp) over every row of the call: the rows the packed pass
@@ -43,7 +52,7 @@ static int launch_tail(const Rows2Args& ra, int BH, hipStream_t stream, bool pla
 }
 template <int NP, int MODE, int W>
 static int launch_select_packed(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  const int tw = sel_tail_width(MODE, ra.T, ra.k_top);
+  const int tw = sel_tail_width(MODE, ra.T, ra.k_top, ra.bias != nullptr);
   int rc;
   if (tw == 32) {
     rc = launch_select_w<NP, MODE, W, uint32_t, 1, 32>(ra, BH, stream, plan);
@@ -64,7 +73,7 @@ static int launch_select_np(const Rows2Args& ra, int BH, hipStream_t stream, boo
   // 64-bit kernel on the rows whose scores do not pack (fb_only: its workgroups without
   // such rows return at once).  The true scores, ELSA and longer rows: the 64-bit kernel.
   if constexpr (NP <= 256) {
-    if (sel_packs(MODE, ra.T) && ra.k_top > 0) {
+    if (sel_packs(MODE, ra.T, ra.bias != nullptr) && ra.k_top > 0 && ra.fb_flags) {
       const int rc = wsel == 2 ? launch_select_packed<NP, MODE, 2>(ra, BH, stream, plan)
                                : launch_select_packed<NP, MODE, 4>(ra, BH, stream, plan);
       if (rc != MXA_OK) return rc;

@@ -488,22 +488,12 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
   wave_lds_sync();
 }
 
-// Selection kernel, four query rows per wave.  El = uint64_t: rows of up to 512 keys,
-// every approximator (a.fb_only: only the rows the packed pass left; a workgroup
-// without such rows returns at once).  El = uint32_t: the packed pass (rows of <= 256
-// keys; half the LDS per row, so more resident waves).
-template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
-__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? MXA_SELP_OCC : NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// One workgroup's work item: head bh, query-row chunk y (rows y * rows_per_wg ...).
+// Returns (on every thread) whether a packed row of the chunk was left for the 64-bit pass.
+template <int NP, int MODE, int kSelWaves, typename El, int QM, int TW>
+__device__ __forceinline__ bool select_item(const Rows2Args& a, unsigned char* smem, int bh, int y) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int bh = blockIdx.x;
-  const int r0 = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r0 + a.rows_per_wg);
-  if (sizeof(El) == 8 && a.fb_only) {
-    int any = 0;
-    for (int r = r0 + (int)threadIdx.x; r < r_end; r += blockDim.x)
-      any |= kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0;
-    if (!__syncthreads_or(any)) return;
-  }
+  const int r0 = y * a.rows_per_wg, r_end = min(a.N, r0 + a.rows_per_wg);
   const SelLds L = sel_lds(MODE, a.T, a.D, a.kst, a.nbd);
   const SelTabs t = sel_stage<MODE>(a, smem, L, bh);
   unsigned char* g0 = smem + L.rows + (size_t)4 * wave * grp_row_bytes(grp_alloc(a.T), NP, sizeof(El));
@@ -515,6 +505,44 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
     }
     sel_rows4<NP, MODE, El, QM, TW>(a, t, g0, bh, rq, r_end, lane);
   }
+  // (packed: a row left for the 64-bit pass has kept_get(row * k) < 0)
+  int left = 0;
+  if (sizeof(El) == 4 && a.k_top > 0)
+    for (int r = r0 + (int)threadIdx.x; r < r_end; r += blockDim.x) left |= kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0;
+  return __syncthreads_or(left) != 0;
+}
+
+// Selection kernel, four query rows per wave.  El = uint64_t: rows of up to 512 keys,
+// every approximator.  El = uint32_t: the packed pass (rows of <= 256 keys; half the LDS
+// per row, so more resident waves); each workgroup flags (a.fb_flags[bh * gy + y]) whether
+// it left rows for the 64-bit pass, which then runs with fb_only: one workgroup per 64
+// flags, taking the flagged items one after another (a call without such rows costs a
+// small grid that exits at once).
+template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? MXA_SELP_OCC : NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (sizeof(El) == 8 && a.fb_only) {
+    __shared__ uint64_t sbits;
+    const int gy = a.fb_gy;
+    const int64_t items = (int64_t)a.B * a.H * gy, i0 = (int64_t)blockIdx.x * 64;
+    if (threadIdx.x < 64) {
+      const bool f = i0 + threadIdx.x < items && a.fb_flags[i0 + threadIdx.x] != 0u;
+      const uint64_t bits = __builtin_amdgcn_ballot_w64(f);
+      if (threadIdx.x == 0) sbits = bits;
+    }
+    __syncthreads();
+    uint64_t bits = sbits;
+    while (bits) {
+      const int i = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      const int64_t item = i0 + i;
+      select_item<NP, MODE, kSelWaves, El, QM, TW>(a, smem, (int)(item / gy), (int)(item % gy));
+      __syncthreads();  // the next item re-stages the tables
+    }
+    return;
+  }
+  const bool left = select_item<NP, MODE, kSelWaves, El, QM, TW>(a, smem, blockIdx.x, blockIdx.y);
+  if (sizeof(El) == 4 && a.fb_flags && threadIdx.x == 0) a.fb_flags[(int64_t)blockIdx.x * gridDim.y + blockIdx.y] = left ? 1u : 0u;
 }
 
 // ---- standalone top-k over rows of a float matrix (mxa_topk) ------------------

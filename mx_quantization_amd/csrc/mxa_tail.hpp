@@ -138,7 +138,12 @@ __device__ __forceinline__ int t_partition(TPtr A, int f, int l, int b, bool act
   using M = TMask<W>;
   const int fa = act ? f : 0, la = act ? l : 4;
   const int mid = fa + ((la - fa) >> 1);
+  // the median candidates and the window in one LDS round trip; the median's iter_swap
+  // is applied to the stop masks (position f is never a stop; position m holds old f)
   const uint32_t xf = A[fa], xa = A[fa + 1], xb = A[mid], xc = A[la - 1];
+  uint32_t K[W];
+#pragma unroll
+  for (int e = 0; e < W; ++e) K[e] = A[b + e];
   const bool ab = lgt(xa, xb), bc = lgt(xb, xc), ac = lgt(xa, xc);
   const bool pick_b = ab ? bc : (!ac && !bc);
   const bool pick_c = ab ? (!bc && ac) : (!ac && bc);
@@ -146,14 +151,11 @@ __device__ __forceinline__ int t_partition(TPtr A, int f, int l, int b, bool act
   uint32_t xm = pick_c ? xc : xa;
   m = pick_b ? mid : m;
   xm = pick_b ? xb : xm;
-  if (act) {  // iter_swap(f, median): this lane's own row, read back below in order
+  if (act) {  // iter_swap(f, median)
     A[fa] = xm;
     A[m] = xf;
   }
   const uint32_t pl = xm | 0xFFu, pr = xm & ~0xFFu;
-  uint32_t K[W];
-#pragma unroll
-  for (int e = 0; e < W; ++e) K[e] = A[b + e];
   M Lm, Rm;
   if constexpr (W > 32) {
     uint32_t Lh = 0, Rh = 0, Ll = 0, Rl = 0;
@@ -169,6 +171,12 @@ __device__ __forceinline__ int t_partition(TPtr A, int f, int l, int b, bool act
     for (int e = W - 1; e >= 0; e -= 2) g_stops2(Lw, Rw, K[e], K[e - 1], pl, pr);
     Lm = Lw;
     Rm = Rw;
+  }
+  {  // position m holds old f now
+    const int em = m - b;
+    const M bm = (uint32_t)em < (uint32_t)W ? (M)1 << em : (M)0;
+    Lm = (Lm & ~bm) | (xf <= pl ? bm : (M)0);
+    Rm = (Rm & ~bm) | (xf >= pr ? bm : (M)0);
   }
   const M rng = act ? (t_low<M>(l - b) & ~t_low<M>(f + 1 - b)) : (M)0;
   Lm &= rng;
@@ -186,18 +194,33 @@ __device__ __forceinline__ int t_partition(TPtr A, int f, int l, int b, bool act
   M SL = Lm & t_low<M>(js);  // the swapping left stops
   const int nsw = t_popc(SL);
   M SR = Rm;  // the nsw highest right stops, taken from the top
-  int t = 0;
-  while (__builtin_amdgcn_ballot_w64(t < nsw) != 0) {
-    if (t < nsw) {
-      const int x = sizeof(M) == 8 ? __ffsll((long long)SL) - 1 : __ffs((int)SL) - 1;
-      const int y = sizeof(M) == 8 ? 63 - __clzll((long long)SR) : 31 - __clz((int)SR);
-      const uint32_t ex = A[b + x], ey = A[b + y];
-      A[b + x] = ey;
-      A[b + y] = ex;
-      SL &= SL - (M)1;
-      SR ^= (M)1 << y;
+  // the swaps four at a time: their positions first, then all reads, then all writes (the
+  // swapping positions are distinct, so one LDS round trip per four swaps)
+  for (int t = 0; __builtin_amdgcn_ballot_w64(t < nsw) != 0; t += 4) {
+    int x[4], y[4];
+    bool on[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      on[i] = t + i < nsw;
+      x[i] = sizeof(M) == 8 ? __ffsll((long long)SL) - 1 : __ffs((int)SL) - 1;
+      y[i] = sizeof(M) == 8 ? 63 - __clzll((long long)SR) : 31 - __clz((int)SR);
+      x[i] = on[i] ? x[i] : 0;
+      y[i] = on[i] ? y[i] : 0;
+      SL = on[i] ? (SL & (SL - (M)1)) : SL;
+      SR = on[i] ? (SR ^ ((M)1 << y[i])) : SR;
     }
-    ++t;
+    uint32_t ex[4], ey[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ex[i] = on[i] ? (uint32_t)A[b + x[i]] : 0u;
+      ey[i] = on[i] ? (uint32_t)A[b + y[i]] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (on[i]) {
+        A[b + x[i]] = ey[i];
+        A[b + y[i]] = ex[i];
+      }
   }
   return b + js;
 }
@@ -330,6 +353,8 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
   if (__builtin_amdgcn_ballot_w64(ph == 3 && m >= 2) != 0) {
     if (m <= 16) {
       if (ph == 3) t_rank<16>(A, m);
+    } else if (m <= 24) {
+      if (ph == 3) t_rank<24>(A, m);
     } else if (m <= 32) {
       if (ph == 3) t_rank<32>(A, m);
     } else {

@@ -59,7 +59,10 @@ constexpr int kGSeg = 16;  // final sort segments queued for one ranking pass
 // NP <= 256, else u16), introsort stack, queue of final segments
 __host__ __device__ constexpr int grp_pbytes(int NP) { return ((NP <= 256 ? 1 : 2) * (NP + 16) + 15) & ~15; }
 __host__ __device__ constexpr size_t grp_row_bytes(int NPA, int NP, int elb = 8) {
-  return (size_t)elb * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg;
+  // packed rows: a stride of 128 mod 256 bytes, so the two rows a 32-lane LDS access
+  // group holds sit half the 64 banks apart (their windows' element reads do not collide)
+  return elb == 4 ? (((size_t)4 * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg + 127) / 256) * 256 + 128
+                  : (size_t)elb * NPA + grp_pbytes(NP) + 4 * kGStk + 4 * kGSeg;
 }
 // (the window widths 16 E are 32, 64, ..., 256, 384, 512, so NPA is one of them)
 __host__ __device__ constexpr int grp_alloc(int T) { return T <= 256 ? (T + 31) & ~31 : (T <= 384 ? 384 : 512); }
