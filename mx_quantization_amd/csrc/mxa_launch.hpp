@@ -22,8 +22,9 @@ inline bool sel_packs(int mode, int T, bool bias) {
 }
 // the prefix the one-lane tail takes over (mxa_tail.hpp), 0 = none: k + 2 <= TW (the
 // introselect's last range and the sort of [0, k-1) lie in it), not partial_sort (k*64 <= T)
+// (k - 1 <= 32: the final stable rank of [0, k-1) in at most 32 registers per lane)
 inline int sel_tail_width(int mode, int T, int k, bool bias) {
-  if (!sel_packs(mode, T, bias) || k <= 0 || (int64_t)k * 64 <= T) return 0;
+  if (!sel_packs(mode, T, bias) || k <= 0 || k > 33 || (int64_t)k * 64 <= T) return 0;
   if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
   return k + 2 <= 64 ? 64 : 0;
 }

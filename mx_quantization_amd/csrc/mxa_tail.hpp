@@ -269,14 +269,15 @@ struct TailArgs {
 };
 
 // one lane per row; a workgroup of kTailWaves waves, each wave's 64 rows' prefixes in LDS
-constexpr int kTailWaves = 4;
+constexpr int kTailWaves = 1;
+constexpr int kTailStk = 12;  // introsort stack entries (depth limit 2 lg(32) + 1 = 11)
 template <int TW>
 __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (64 * kTailWaves) + threadIdx.x;
-  const TPtr A{(tl32*)(lu32*)(smem) + (size_t)wave * 64 * (TW + 16) + lane};
-  const TPtr stk = A + TW;  // introsort stack: 16 entries after the prefix
+  const TPtr A{(tl32*)(lu32*)(smem) + (size_t)wave * 64 * (TW + kTailStk) + lane};
+  const TPtr stk = A + TW;  // introsort stack: kTailStk entries after the prefix
   uint32_t st = 0u;
   if (row < a.rows) {
     const uint32_t* src = a.rec + row * tail_rec_words(TW);
@@ -350,15 +351,13 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
     }
   }
   // std::sort's final insertion sort = a stable rank of [0, m) (segments mutually ordered)
-  if (__builtin_amdgcn_ballot_w64(ph == 3 && m >= 2) != 0) {
+  if (__builtin_amdgcn_ballot_w64(ph == 3 && m >= 2) != 0) {  // (m <= 32: sel_tail_width)
     if (m <= 16) {
       if (ph == 3) t_rank<16>(A, m);
     } else if (m <= 24) {
       if (ph == 3) t_rank<24>(A, m);
-    } else if (m <= 32) {
-      if (ph == 3) t_rank<32>(A, m);
     } else {
-      if (ph == 3) t_rank<TW>(A, m);
+      if (ph == 3) t_rank<32>(A, m);
     }
   }
   if (!pend) return;
@@ -379,6 +378,6 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
   }
 }
 
-__host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * (TW + 16) * 4; }
+__host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * (TW + kTailStk) * 4; }
 
 }  // namespace mxa
