@@ -256,11 +256,15 @@ def _unique_kernel(d, stage):
 
 
 def stage_of_kernel(name):
-    if "select_q_kernel" in name:  # the packed-element selection kernel
-        return "select"
-    if "select_kernel" in name:  # the 64-bit one: rows the packed kernel leaves, true scores, ELSA
-        return "select_fb"
-    if "finish_kernel" in name or "finish16_kernel" in name or "dense_rows_kernel" in name:
+    """The bench stage (or selection sub-stage) of a kernel instantiation: the selection
+    stage's HIP events cover the packed selection kernel ("select"), the one-lane top-k
+    tail ("select_tail") and the 64-bit kernel ("select_fb": the rows the packed pass
+    leaves, or every row where the scores do not pack)."""
+    if "topk_tail_kernel" in name:
+        return "select_tail"
+    if "select_kernel" in name:
+        return "select" if "unsigned int" in name else "select_fb"
+    if any(f in name for f in ("finish_kernel", "finish16_kernel", "finish_qk_kernel", "dense_rows_kernel")):
         return "finish"
     if "attn_prep_kernel" in name:
         return "prep"

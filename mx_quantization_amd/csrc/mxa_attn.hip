@@ -70,7 +70,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 // workspace regions, 256-B aligned
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
-  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail, fbf;
+  int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail, fbf, mask;
   int64_t xc, xs, slow;  // fused qkv projection: x codes / exponents, slow-head list
   int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
                               // copy (D % 32 != 0 only), the GEMM's fp64 wave list
@@ -136,6 +136,11 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
     L.tail = take(tw ? qrows * (int64_t)tail_rec_words(tw) * 4 : 0);
     L.fbf = take(pk ? BH * (int64_t)((p->N + 15) / 16) * 4 : 0);
   }
+  // the prune-mask words for the MFMA finishing kernel when the caller takes none
+  // (reserved whatever mask_out is: the size must not depend on it)
+  L.mask = take(p->top_k && finish_qk_wanted(p->k_top, p->T, L.nbd, pj && proj_codes_direct(p))
+                    ? qrows * (int64_t)L.ntb * 4
+                    : 0);
   if (xq) {
     const int64_t nbk = (xq->C + 31) / 32, tokens = (int64_t)p->B * p->N;
     L.xc = take(tokens * nbk * 32);
@@ -394,6 +399,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   r2.tail_rec = reinterpret_cast<uint32_t*>(ws + L.tail);
   r2.fb_flags = reinterpret_cast<uint32_t*>(ws + L.fbf);
   const bool direct = pj && proj_codes_direct(&pp);
+  if (topk && !r2.mask_out && finish_qk_wanted(r2.k_top, r2.T, r2.nbd, direct))
+    r2.mask_out = reinterpret_cast<uint32_t*>(ws + L.mask);
   if (direct) {  // the finishing kernel writes the proj's input codes
     r2.xo_codes = reinterpret_cast<int8_t*>(ws + L.yc);
     r2.xo_exps = reinterpret_cast<int16_t*>(ws + L.ys);

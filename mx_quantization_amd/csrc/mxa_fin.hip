@@ -187,6 +187,10 @@ static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
 }
 
 static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  if (finish_qk_wanted(ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr)) {
+    if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish_qk_x1(ra, BH, stream, plan);
+    return launch_finish_qk_x0(ra, BH, stream, plan);
+  }
   // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k
   // (DiT's 154): the 32-row kernel (measured: DiT-XL/2 0.35 ms there vs 0.39 with
   // 16-row tiles of sixteen lanes per row)

@@ -46,6 +46,17 @@ inline int launch_select_mode(const Rows2Args& ra, int mode, int BH, hipStream_t
     default: return launch_select_p6(ra, BH, stream, plan);
   }
 }
+// the finishing kernel with the scores of every key on MFMA (mxa_finish_qk.hpp): k a large
+// share of T (above the 16-row gather kernel's k <= 64), T <= 256 (the scores of a row in
+// registers); not with the proj Linear's MX input codes (xo).  It reads the selection's
+// prune-mask words (the caller's mask_out, else a workspace copy), not the kept indices.
+#ifndef MXA_FQ_MINK
+#define MXA_FQ_MINK 65
+#endif
+inline bool finish_qk_wanted(int k, int T, int nbd, bool xo) { return k >= MXA_FQ_MINK && T <= 256 && nbd <= 4 && !xo; }
+// its launches (mxa_fin_qk.hip): float32 inputs and scores (x0), float16 / bfloat16 (x1)
+int launch_finish_qk_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+int launch_finish_qk_x1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
 // the row kernel of the path: finishing kernel (top-k) or dense row kernel (mxa_fin.hip)
 int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan);
 // fused qkv projection kernel (mxa_proj.hip)

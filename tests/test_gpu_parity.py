@@ -434,11 +434,14 @@ def test_expred_paths_vs_oracle(M, D, N, T, k):
         _check_vs_oracle(got, r, name)
 
 
-def test_expred_special_rows(M):
+@pytest.mark.parametrize("k", [20, 100])
+def test_expred_special_rows(M, k):
     """Zero K rows (exponent -126 blocks), a wide exponent spread, NaN / Inf
-    inputs, rows whose true scores overflow, all-zero query rows."""
+    inputs, rows whose true scores overflow, all-zero query rows; k on the gather
+    finishing kernel (20) and on the MFMA one (100: every key's exact epilogue, its fp64
+    and NaN branches)."""
     rng = np.random.default_rng(5)
-    B, H, N, T, D, k = 2, 4, 197, 197, 64, 20
+    B, H, N, T, D = 2, 4, 197, 197, 64
     q = rng.standard_normal((B, H, N, D), dtype=np.float32)
     kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
     v = rng.standard_normal((B, H, T, D), dtype=np.float32)

@@ -121,8 +121,10 @@ def test_bench_byte_and_op_accounting():
 
 def test_hbm_traffic_kernel_names_map_to_bench_stages():
     ht = _load_hbm_traffic()
-    assert ht.stage_of("void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)") == "select"
-    assert ht.stage_of("void mxa::select_kernel<256, 3, 2>(mxa::Rows2Args)") == "select_fb"
+    assert ht.stage_of("void mxa::select_kernel<256, 3, 2, unsigned int, 1, 64>(mxa::Rows2Args)") == "select"
+    assert ht.stage_of("void mxa::select_kernel<256, 3, 2, unsigned long, 0, 0>(mxa::Rows2Args)") == "select_fb"
+    assert ht.stage_of("void mxa::topk_tail_kernel<64>(mxa::TailArgs)") == "select_tail"
+    assert ht.stage_of("void mxa::finish_qk_kernel<3, 8, false>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("void mxa::finish_kernel<2, 2>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("void mxa::dense_rows_kernel<4>(mxa::Rows2Args)") == "finish"
     assert ht.stage_of("mxa::attn_prep_kernel(mxa::RowsPrepArgs, mxa::RowsPrepArgs, mxa::ColsPrepArgs, unsigned int, "
@@ -143,8 +145,8 @@ def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
     DiT's select_kernel<256,3,4> dispatches: per-instantiation keys keep them apart, and a
     stage with two instantiations in one run gets no traffic number at all."""
     ht = _load_hbm_traffic()
-    deit, dit = ("void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)",
-                 "void mxa::select_q_kernel<256, 3, 4, 16, true>(mxa::Rows2Args)")
+    deit, dit = ("void mxa::select_kernel<256, 3, 2, unsigned int, 1, 64>(mxa::Rows2Args)",
+                 "void mxa::select_kernel<256, 3, 4, unsigned int, 0, 0>(mxa::Rows2Args)")
     fin = "void mxa::finish_kernel<2, 12, true>(mxa::Rows2Args)"
     rows = []
     for name, kib_f, kib_w, n in ((deit, 10.0, 143250.0, 7), (dit, 20.0, 473145.0, 3), (fin, 100.0, 200.0, 7)):
@@ -156,6 +158,23 @@ def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
     assert out["kernels"][dit]["write_bytes"] == 473145.0 * 1024
     assert out["kernels"][deit]["traffic_bytes"] == (2 * 10.0 + 143250.0) * 1024
     assert "select" not in out["stages"] and sorted(out["ambiguous"]["select"]) == sorted([deit, dit])
+
+
+def test_hbm_traffic_select_stage_sums_its_kernels():
+    """The selection stage's HIP events span the packed kernel, the one-lane tail and the
+    64-bit pass: its traffic per launch is the sum of the three."""
+    ht = _load_hbm_traffic()
+    names = {"void mxa::select_kernel<256, 3, 2, unsigned int, 1, 64>(mxa::Rows2Args)": 100.0,
+             "void mxa::topk_tail_kernel<64>(mxa::TailArgs)": 10.0,
+             "void mxa::select_kernel<256, 3, 2, unsigned long, 0, 0>(mxa::Rows2Args)": 1.0}
+    rows = []
+    for name, kib in names.items():
+        for _ in range(3):
+            rows.append({"Kernel_Name": name, "Counter_Name": "FETCH_SIZE", "Counter_Value": str(kib)})
+            rows.append({"Kernel_Name": name, "Counter_Name": "WRITE_SIZE", "Counter_Value": str(kib)})
+    out = ht.combine(ht.per_kernel(rows, "FETCH_SIZE"), ht.per_kernel(rows, "WRITE_SIZE"))
+    assert out["stages"]["select"] == 3 * 111.0 * 1024
+    assert out["stages"]["select_parts"]["select_tail"] == 3 * 10.0 * 1024
     assert out["stages"]["finish"] == (2 * 100.0 + 200.0) * 1024
     # a run with one instantiation per stage maps every stage
     one = ht.combine(ht.per_kernel(rows[:14], "FETCH_SIZE"), ht.per_kernel(rows[:14], "WRITE_SIZE"))

@@ -8,7 +8,7 @@ T=${TAG:-p}
 for c in ${CFGS:-deit_base dit_xl2}; do
   rm -rf gpurun_out/prof_${T}_$c
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_$c -o run --output-format csv -- \
-    python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-parity --lines main > gpurun_out/prof_${T}_$c.json 2> gpurun_out/prof_${T}_$c.err || { tail -5 gpurun_out/prof_${T}_$c.err; exit 1; }
+    python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-parity --lines ${LINES:-main} > gpurun_out/prof_${T}_$c.json 2> gpurun_out/prof_${T}_$c.err || { tail -5 gpurun_out/prof_${T}_$c.err; exit 1; }
   f=$(find gpurun_out/prof_${T}_$c -name "*kernel_stats.csv" | head -1)
   echo "== $c"; python3 -c "
 import csv

@@ -25,11 +25,12 @@ import sys
 
 
 def stage_of(kernel):
-    if "select_q_kernel" in kernel:  # the packed-element selection kernel
-        return "select"
-    if "select_kernel" in kernel:  # the 64-bit one: rows the packed kernel leaves, true scores, ELSA
-        return "select_fb"
-    if "finish_kernel" in kernel or "finish16_kernel" in kernel or "dense_rows_kernel" in kernel:
+    """bench.py stage_of_kernel (kept in step by tests/test_multiproc_cpu.py)."""
+    if "topk_tail_kernel" in kernel:
+        return "select_tail"
+    if "select_kernel" in kernel:
+        return "select" if "unsigned int" in kernel else "select_fb"
+    if any(f in kernel for f in ("finish_kernel", "finish16_kernel", "finish_qk_kernel", "dense_rows_kernel")):
         return "finish"
     if "attn_prep_kernel" in kernel:
         return "prep"
@@ -38,6 +39,10 @@ def stage_of(kernel):
     if "mx_gemm_kernel" in kernel or "mx_gemm_dig_kernel" in kernel:
         return "proj_linear"
     return None
+
+
+# the selection stage's HIP events span its sub-stages: its traffic is their sum
+STAGE_PARTS = {"select": ("select", "select_tail", "select_fb")}
 
 
 def per_kernel(rows, counter):
@@ -83,6 +88,11 @@ def combine(fetch, write):
             stages[st] = kernels[names[0]]["traffic_bytes"]
         else:
             ambiguous[st] = names
+    for st, parts in STAGE_PARTS.items():  # whole-stage sums: one instantiation per part
+        if any(p in ambiguous for p in parts) or not any(p in stages for p in parts):
+            continue
+        stages[st + "_parts"] = {p: stages[p] for p in parts if p in stages}
+        stages[st] = sum(stages[p] for p in parts if p in stages)
     return {"kernels": kernels, "stages": stages, "ambiguous": ambiguous,
             "note": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes, gfx950 correction), "
                     "per launch, averaged over the dispatches of ONE kernel instantiation"}
