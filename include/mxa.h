@@ -128,6 +128,18 @@ int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
              int64_t* out_idx, void* out_vals, uint32_t* out_mask, int32_t dtype, hipStream_t stream);
 
 /*
+ * mxa_topk with a device workspace (the same results): rows of <= 256 values go through
+ * the packed 32-bit selection pass and the one-lane tail (the fused op's selection
+ * engine), which stage per-row state in the workspace.  mxa_topk_workspace_bytes:
+ * the bytes it needs (0: no workspace path for this shape -- mxa_topk_ws then runs
+ * mxa_topk; -1: invalid arguments).  workspace: 16-B aligned device memory.
+ */
+int64_t mxa_topk_workspace_bytes(int64_t rows, int32_t n, int32_t k);
+int mxa_topk_ws(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k,
+                int64_t* out_idx, void* out_vals, uint32_t* out_mask, int32_t dtype,
+                void* workspace, int64_t workspace_bytes, hipStream_t stream);
+
+/*
  * The fused hot path: MXINT8 true scores, approximate scores, top-k prune,
  * softmax over the kept scores, MXINT8 P.V -- the mx_quant branch of
  *   QuantizedAttention.forward  workloads/deit/scripts/main.py:100-152

@@ -69,6 +69,8 @@ _SIGS = {
     "mxa_quantize_bfloat": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp]),
     "mxa_approx_values": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp]),
     "mxa_topk": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "mxa_topk_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32]),
+    "mxa_topk_ws": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp]),
     "mxa_attention_workspace_bytes": (c_i64, [ctypes.POINTER(AttnParams)]),
     "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),

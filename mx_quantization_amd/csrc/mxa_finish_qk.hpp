@@ -315,7 +315,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             }
             // a dropped key: -inf (the kept bit as an all-ones / zero mask, one bit select)
             const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)kw[blk >> 2], 8 * (blk & 3) + 4 * t + i, 1);
-            v[blk][4 * t + i] = __uint_as_float((__float_as_uint(s) & m) | (0xFF800000u & ~m));
+            uint32_t sv;
+            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(sv) : "v"(m), "v"(__float_as_uint(s)), "v"(0xFF800000u));
+            v[blk][4 * t + i] = __uint_as_float(sv);
             mx = fmaxf(mx, v[blk][4 * t + i]);
           }
           // one key tile's MFMAs and epilogue at a time: hoisting the later tiles' MFMAs
@@ -343,7 +345,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
           v[blk][j] = __builtin_amdgcn_exp2f((v[blk][j] - mx) * 1.4426950408889634f);
           sum += v[blk][j];
         }
-    if (mx == -INFINITY) {
+    if (__builtin_amdgcn_ballot_w64(mx == -INFINITY)) {  // wave-uniform branch: rare rows only
+      if (mx == -INFINITY)
 #pragma unroll
       for (int blk = 0; blk < NTB; ++blk)
         if (blk < ntb)
@@ -359,6 +362,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     sum = fq_fsum4(sum);
     const bool nan_sum = sum != sum;
+    const bool any_nan = __builtin_amdgcn_ballot_w64(nan_sum) != 0;  // wave-uniform: rare rows only
     // p = v / sum correctly rounded without a division per element (Markstein: y = RN(1/sum),
     // q = RN(v y), r = v - q sum exact by fma, RN(q + r y) = RN(v / sum); v in [0, 1],
     // sum in [1, T]: no overflow, and subnormal p only where the block is negligible)
@@ -380,10 +384,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
           const float q1 = __builtin_fmaf(__builtin_fmaf(-q0, sum, v[blk][j]), rs, q0);
           v[blk][j] = kRound ? round_dt(round_bfloat(q1, a.bfloat, kRoundNearest, 1, sdt), sdt) : q1;
         }
-        if (nan_sum)
+        if (any_nan)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (!kept(blk, j)) v[blk][j] = 0.0f;
+            if (nan_sum && !kept(blk, j)) v[blk][j] = 0.0f;
         uint32_t bm = 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) bm = max(bm, __float_as_uint(v[blk][j]) & 0x7FFFFFFFu);

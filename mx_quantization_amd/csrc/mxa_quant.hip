@@ -346,6 +346,75 @@ __global__ __launch_bounds__(256) void approx_values_kernel(ApproxArgs a) {
   store_dt(a.out, row * a.ld_out + c, round_dt(out, dt), dt);
 }
 
+// approx_values_kernel for float32 rows of whole 32-element blocks at 16-B aligned
+// strides: eight lanes per block, four elements per lane (one float4 load and store),
+// the block maxima over the eight lanes by DPP, 32-bit index math -- the same values
+// (it is HBM-bound: 8 bytes per element)
+template <int OPK>
+__global__ __launch_bounds__(256) void approx_values_v4_kernel(ApproxArgs a) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t gid = t >> 3, nb = (uint32_t)(a.d >> 5);
+  const int sub = (int)(t & 7u);
+  const bool live = gid < (uint32_t)a.rows * nb;  // every lane takes part in the DPP steps
+  const uint32_t row = live ? gid / nb : 0u, blk = live ? gid - row * nb : 0u;
+  const int c = (int)blk * 32 + 4 * sub;
+  float xin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (live) {
+    const float4 x4 = *reinterpret_cast<const float4*>(static_cast<const float*>(a.x) + (int64_t)row * a.ld_x + c);
+    xin[0] = x4.x; xin[1] = x4.y; xin[2] = x4.z; xin[3] = x4.w;
+    if (a.bfloat != 0 && a.bfloat != 32)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xin[i] = round_bfloat(xin[i], a.bfloat, kRoundNearest, 1);
+  }
+  auto umax = [](uint32_t p, uint32_t q) { return p > q ? p : q; };
+  uint32_t mb = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mb = umax(mb, __float_as_uint(xin[i]) & 0x7FFFFFFFu);
+  mb = oct_reduce(mb, umax);
+  int e_raw;
+  const int es = scale_exponent(mb, 127, &e_raw);
+  const bool nanblk = es == kExpNaN;
+  const bool flush = a.flush && !(e_raw != kExpNaN && e_raw > -127);
+  int cd[4];
+  uint32_t mc = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float xv = flush ? xin[i] * 0.0f : xin[i];
+    cd[i] = nanblk ? 0 : (int)round_code(xv, es, 8, kRoundNearest);
+    mc = umax(mc, (uint32_t)(cd[i] < 0 ? -cd[i] : cd[i]));
+  }
+  const int maxc = (int)oct_reduce(mc, umax);
+  const int eA = nanblk ? kExpNaN : (maxc == 0 ? -126 : floor_log2_pos((float)maxc * pow2f(es - 6)));
+  if (!live) return;
+  float out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (nanblk) {
+      out[i] = OPK == MXA_OP_TRUE_EX ? 1.0f : __uint_as_float(0x7FC00000u);
+    } else if (OPK == MXA_OP_MXINT4) {
+      const float xv = flush ? xin[i] * 0.0f : xin[i];
+      out[i] = (round_code(xv, es, 4, kRoundNearest) * 0.25f) * pow2f(es);
+    } else {
+      const float mxv = ((float)cd[i] * pow2f(-6)) * pow2f(es);
+      if (OPK == MXA_OP_SIGN) {
+        out[i] = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(eA);
+      } else if (OPK == MXA_OP_EXION) {
+        const int m = exion_m(cd[i] << (es - eA));
+        const float sg = cd[i] > 0 ? 1.0f : (cd[i] < 0 ? -1.0f : 0.0f);
+        out[i] = ((sg * (float)eA) * (float)(m < 0 ? -m : m)) / 64.0f;
+      } else if (OPK == MXA_OP_TRUE_EX) {
+        const float am = fabsf(mxv);
+        const int te = am > 0.0f ? floor_log2_pos(am) : 0;
+        out[i] = (mxv < 0.0f ? -1.0f : 1.0f) * pow2f(te);
+      } else {
+        out[i] = mxv;
+      }
+    }
+  }
+  *reinterpret_cast<float4*>(static_cast<float*>(a.out) + (int64_t)row * a.ld_out + c) =
+      make_float4(out[0], out[1], out[2], out[3]);
+}
+
 // quantize_mx along a contiguous axis in 32-element blocks (the mx ops' axes=[-1] case):
 // one lane per element, the block max by lane shuffles -- quantize_mx_kernel's result
 __global__ __launch_bounds__(256) void quantize_mx_row32_kernel(QuantArgs a) {
@@ -448,7 +517,20 @@ extern "C" int mxa_approx_values(const void* x, void* out, int64_t rows, int32_t
   ApproxArgs a{};
   a.x = x; a.out = out; a.rows = rows; a.d = d; a.ld_x = ld_x; a.ld_out = ld_out;
   a.op_kind = op_kind; a.flush = flush_subnormals; a.bfloat = bfloat; a.dt = dtype;
-  const int64_t n = rows * ((d + 31) / 32) * 32;  // one lane per element of the padded blocks
+  const int64_t nbk = rows * ((d + 31) / 32);
+  if (dtype == MXA_DT_F32 && d % 32 == 0 && ld_x % 4 == 0 && ld_out % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0 &&
+      nbk * 8 < ((int64_t)1 << 31)) {  // eight lanes per block, float4 in and out
+    const dim3 grid((unsigned)((nbk * 8 + 255) / 256));
+    switch (op_kind) {
+      case MXA_OP_SIGN: hipLaunchKernelGGL(approx_values_v4_kernel<MXA_OP_SIGN>, grid, dim3(256), 0, stream, a); break;
+      case MXA_OP_EXION: hipLaunchKernelGGL(approx_values_v4_kernel<MXA_OP_EXION>, grid, dim3(256), 0, stream, a); break;
+      case MXA_OP_MXINT4: hipLaunchKernelGGL(approx_values_v4_kernel<MXA_OP_MXINT4>, grid, dim3(256), 0, stream, a); break;
+      case MXA_OP_TRUE_EX: hipLaunchKernelGGL(approx_values_v4_kernel<MXA_OP_TRUE_EX>, grid, dim3(256), 0, stream, a); break;
+      default: hipLaunchKernelGGL(approx_values_v4_kernel<MXA_OP_MXINT8>, grid, dim3(256), 0, stream, a); break;
+    }
+    return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+  }
+  const int64_t n = nbk * 32;  // one lane per element of the padded blocks
   if (n / 256 >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(approx_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;

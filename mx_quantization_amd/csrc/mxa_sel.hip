@@ -124,21 +124,69 @@ static int launch_topk_wave(const GrpTopkArgs& ga, hipStream_t stream) {
   hipLaunchKernelGGL(topk_wave_kernel<NP>, dim3((unsigned)((ga.rows + 3) / 4)), dim3(256), lds, stream, ga);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
-template <int NP>
-static int launch_topk_grp(const GrpTopkArgs& ga, unsigned grid, hipStream_t stream) {
-  const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_grp_kernel<NP>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  hipLaunchKernelGGL(topk_grp_kernel<NP>, dim3(grid), dim3(256), lds, stream, ga);
+template <int NP, typename El = uint64_t, int QM = 0, int TW = 0>
+static int launch_topk_grp(const GrpTopkArgs& ga, const TopkWs& w, unsigned grid, hipStream_t stream) {
+  const size_t lds = (size_t)16 * grp_row_bytes(grp_alloc(ga.n), NP, sizeof(El));
+  const void* fn = reinterpret_cast<const void*>(&topk_grp_kernel<NP, El, QM, TW>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
+  hipLaunchKernelGGL((topk_grp_kernel<NP, El, QM, TW>), dim3(grid), dim3(256), lds, stream, ga, w);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
+}
+
+// the workspace path of the standalone top-k: the packed pass for rows of <= 256 values
+// (mxa_select.hpp topk_rows16), the one-lane tail for k <= 33 (mxa_tail.hpp), the 64-bit
+// pass over the rows it leaves
+static int topk_ws_tw(int n, int k) {
+  if (k <= 0 || k > 33 || (int64_t)k * 64 <= n) return 0;
+  if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
+  return k + 2 <= 64 ? 64 : 0;
+}
+static bool topk_ws_packs(int n, int k) { return n <= 256 && k > 0; }
+static int64_t topk_ws_bytes(int64_t rows, int n, int k) {
+  if (!topk_ws_packs(n, k)) return 0;
+  const int tw = topk_ws_tw(n, k);
+  const int64_t nwg = (rows + 15) / 16;
+  return ((nwg * 4 + 255) / 256) * 256 + (tw ? rows * (int64_t)tail_rec_words(tw) * 4 : 0);
+}
+template <int NP, int TW>
+static int launch_topk_packed(const GrpTopkArgs& ga, const TopkWs& w, unsigned grid, hipStream_t stream) {
+  const int m = ga.k - 1;
+  int rc;
+  if (TW > 0 || m <= 64) rc = launch_topk_grp<NP, uint32_t, 1, TW>(ga, w, grid, stream);
+  else rc = launch_topk_grp<NP, uint32_t, 2, 0>(ga, w, grid, stream);
+  if (rc) return rc;
+  if constexpr (TW > 0) {
+    TailArgs ta{w.tail_rec, ga.rows, ga.k, (ga.n + 31) / 32, ga.out_idx, nullptr, ga.out_mask, ga.vals, ga.ld, ga.dt,
+                ga.out_vals};
+    const size_t lds = tail_lds(TW);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tail_kernel<TW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return MXA_ERR_LAUNCH;
+    hipLaunchKernelGGL(topk_tail_kernel<TW>, dim3((unsigned)((ga.rows + 64 * kTailWaves - 1) / (64 * kTailWaves))),
+                       dim3(64 * kTailWaves), lds, stream, ta);
+    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+  }
+  TopkWs f = w;
+  f.fb_only = 1;
+  return launch_topk_grp<NP>(ga, f, (unsigned)((w.n_wg + 63) / 64), stream);
+}
+
+static int topk_check(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx, int32_t dtype) {
+  if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
+  if (dtype != kF32 && dtype != kF16 && dtype != kBF16) return MXA_ERR_ARG;
+  if (n > kWMaxN) return MXA_ERR_UNSUPPORTED;
+  return MXA_OK;
+}
+
+extern "C" int64_t mxa_topk_workspace_bytes(int64_t rows, int32_t n, int32_t k) {
+  if (rows < 0 || n <= 0 || k < 0 || k > n) return -1;
+  return topk_ws_bytes(rows, n, k);
 }
 
 extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
                         void* out_vals, uint32_t* out_mask, int32_t dtype, hipStream_t stream) {
-  if (!vals || !out_idx || rows < 0 || n <= 0 || ld < n || k < 0 || k > n) return MXA_ERR_ARG;
-  if (dtype != kF32 && dtype != kF16 && dtype != kBF16) return MXA_ERR_ARG;
-  if (n > kWMaxN) return MXA_ERR_UNSUPPORTED;
+  int rc = topk_check(vals, rows, n, ld, k, out_idx, dtype);
+  if (rc) return rc;
   if (rows == 0) return MXA_OK;
   if (k == 0) {
     if (out_mask) return hipMemsetAsync(out_mask, 0, (size_t)rows * ((n + 31) / 32) * 4, stream) == hipSuccess
@@ -148,15 +196,38 @@ extern "C" int mxa_topk(const void* vals, int64_t rows, int32_t n, int64_t ld, i
   const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
   // rows of 513..1024 (PixArt 512x512 self-attention): one wave per row (mxa_topk_wave.hpp);
   // shorter rows: four rows per wave (mxa_topk_grp.hpp, measured faster)
-  if (n > 512) {
-    if (n <= 256) return launch_topk_wave<256>(ga, stream);
-    if (n <= 512) return launch_topk_wave<512>(ga, stream);
-    return launch_topk_wave<1024>(ga, stream);
-  }
+  if (n > 512) return launch_topk_wave<1024>(ga, stream);
   const unsigned grid = (unsigned)((rows + 15) / 16);
-  if (n <= 128) return launch_topk_grp<128>(ga, grid, stream);
-  if (n <= 256) return launch_topk_grp<256>(ga, grid, stream);
-  return launch_topk_grp<512>(ga, grid, stream);
+  const TopkWs w{};
+  if (n <= 128) return launch_topk_grp<128>(ga, w, grid, stream);
+  if (n <= 256) return launch_topk_grp<256>(ga, w, grid, stream);
+  return launch_topk_grp<512>(ga, w, grid, stream);
+}
+
+extern "C" int mxa_topk_ws(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx,
+                           void* out_vals, uint32_t* out_mask, int32_t dtype, void* workspace, int64_t workspace_bytes,
+                           hipStream_t stream) {
+  int rc = topk_check(vals, rows, n, ld, k, out_idx, dtype);
+  if (rc) return rc;
+  const int64_t need = topk_ws_bytes(rows, n, k);
+  if (rows == 0 || need == 0) return mxa_topk(vals, rows, n, ld, k, out_idx, out_vals, out_mask, dtype, stream);
+  if (!workspace || workspace_bytes < need) return MXA_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(workspace) & 15u) != 0) return MXA_ERR_ARG;
+  const GrpTopkArgs ga{vals, rows, ld, n, k, out_idx, out_vals, out_mask, dtype};
+  TopkWs w{};
+  w.n_wg = (rows + 15) / 16;
+  w.fb_flags = static_cast<uint32_t*>(workspace);
+  w.tail_rec = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) + ((w.n_wg * 4 + 255) / 256) * 256);
+  const unsigned grid = (unsigned)w.n_wg;
+  const int tw = topk_ws_tw(n, k);
+  if (n <= 128) {
+    if (tw == 64) return launch_topk_packed<128, 64>(ga, w, grid, stream);
+    if (tw == 32) return launch_topk_packed<128, 32>(ga, w, grid, stream);
+    return launch_topk_packed<128, 0>(ga, w, grid, stream);
+  }
+  if (tw == 64) return launch_topk_packed<256, 64>(ga, w, grid, stream);
+  if (tw == 32) return launch_topk_packed<256, 32>(ga, w, grid, stream);
+  return launch_topk_packed<256, 0>(ga, w, grid, stream);
 }
 
 #endif  // MXA_SEL_PART == 0

@@ -556,22 +556,68 @@ struct GrpTopkArgs {
   int dt;
 };
 
-template <int NP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ? 4 : 2, 8))) void topk_grp_kernel(GrpTopkArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// the standalone top-k's workspace path (mxa_topk_ws): the packed pass's tail records and
+// per-workgroup flags
+struct TopkWs {
+  uint32_t* tail_rec;  // [rows][tail_rec_words(TW)] (TW > 0)
+  uint32_t* fb_flags;  // per packed workgroup: rows left for the 64-bit pass
+  int64_t n_wg;        // packed workgroups (fb pass: flags to read)
+  int fb_only;         // 64-bit pass over the flagged workgroups' rows with out_idx[row * k] < 0
+};
+
+// sixteen rows (four per wave) from row0: El = uint64_t any row (fb: only rows whose first
+// index is -1); El = uint32_t the packed pass (a row whose values do not leave the key's low
+// byte free gets first index -1 and is left for the 64-bit pass; TW > 0: rows whose remaining
+// work fits the tail's prefix are handed to topk_tail_kernel).  Returns (on every thread)
+// whether a row was left.
+template <int NP, typename El, int QM, int TW>
+__device__ __forceinline__ bool topk_rows16(const GrpTopkArgs& a, const TopkWs& w, unsigned char* smem, int64_t row0,
+                                            bool fb) {
+  constexpr bool kPacked = sizeof(El) == 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gi = lane >> 4, gl = lane & 15;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * 4 + gi;
-  const bool valid = row < a.rows;
+  const int64_t row = row0 + 4 * wave + gi;
+  bool valid = row < a.rows;
+  if (fb && valid) valid = a.out_idx[row * a.k] < 0;
   const int npa = grp_alloc(a.n);
-  const GrpRow<> g = carve_grp(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP), npa, NP);
+  const GrpRow<El> g = carve_grp<El>(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP, sizeof(El)), npa, NP);
   const int64_t src = (valid ? row : 0) * a.ld;
+  uint32_t bad = 0u;
   if (valid)
-    for (int j = gl; j < a.n; j += 16) g.A[j] = pack_ki(order_key(load_dt(a.vals, src + j, a.dt)), (uint32_t)j);
+    for (int j = gl; j < a.n; j += 16) {
+      const float v = load_dt(a.vals, src + j, a.dt);
+      if constexpr (kPacked) {
+        bad |= q_bad_bits(v);
+        g.A[j] = qelem(order_key(v), (uint32_t)j);
+      } else {
+        g.A[j] = pack_ki(order_key(v), (uint32_t)j);
+      }
+    }
+  bool left = false;
+  if constexpr (kPacked) {
+    const uint64_t bw = __builtin_amdgcn_ballot_w64(bad != 0u);
+    if (valid && ((bw >> (16 * gi)) & 0xFFFFull) != 0) {
+      if (gl == 0) a.out_idx[row * a.k] = -1;
+      valid = false;
+      left = true;
+    }
+  }
   wave_lds_sync();
-  grp_topk<NP>(g, a.n, a.k, valid, gl);
+  GrpHand hand{0u, false};
+  grp_topk<NP, El, QM, TW>(g, a.n, a.k, valid, gl, &hand);
+  if (TW > 0 && hand.on) {  // the row's state and prefix to the tail kernel
+    uint32_t* rec = w.tail_rec + row * tail_rec_words(TW);
+    if (gl == 0) {
+      rec[0] = hand.state | kTailPending;
+      a.out_idx[row * a.k] = 0;
+    }
+    for (int p = gl; p < TW; p += 16) rec[4 + p] = (uint32_t)g.A[p];
+    valid = false;
+  } else if (TW > 0 && row < a.rows && !fb) {  // not the tail's
+    if (gl == 0) w.tail_rec[row * tail_rec_words(TW)] = 0u;
+  }
   if (valid) {
     for (int p = gl; p < a.k; p += 16) {
-      const uint32_t ix = (uint32_t)g.A[p];
+      const uint32_t ix = GEl<El>::idx(g.A[p]);
       a.out_idx[row * a.k + p] = (int64_t)ix;
       if (a.out_vals) store_dt(a.out_vals, row * a.k + p, load_dt(a.vals, src + ix, a.dt), a.dt);
     }
@@ -579,17 +625,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NP <= 256 ?
   if (a.out_mask) {
     const int ntw = (a.n + 31) / 32;
     lu32* mw = g.stk;
-    if (gl < ntw) mw[gl] = 0u;
+    for (int i = gl; i < ntw; i += 16) mw[i] = 0u;
     wave_lds_sync();
     if (valid)
       for (int p = gl; p < a.k; p += 16) {
-        const uint32_t ix = (uint32_t)g.A[p];
+        const uint32_t ix = GEl<El>::idx(g.A[p]);
         atomicOr((uint32_t*)(mw + (ix >> 5)), 1u << (ix & 31));
       }
     wave_lds_sync();
     if (valid)
-      for (int w = gl; w < ntw; w += 16) a.out_mask[row * ntw + w] = mw[w];
+      for (int i = gl; i < ntw; i += 16) a.out_mask[row * ntw + i] = mw[i];
   }
+  wave_lds_sync();
+  return __syncthreads_or(left ? 1 : 0) != 0;
+}
+
+// El = uint64_t: every row (w.fb_only: one workgroup per 64 flags of the packed pass, taking
+// the flagged workgroups' left rows); El = uint32_t: the packed pass, flagging per workgroup
+template <int NP, typename El = uint64_t, int QM = 0, int TW = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? 5 : NP <= 256 ? 4 : 2, 8))) void topk_grp_kernel(GrpTopkArgs a, TopkWs w) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (sizeof(El) == 8 && w.fb_only) {
+    __shared__ uint64_t sbits;
+    const int64_t i0 = (int64_t)blockIdx.x * 64;
+    if (threadIdx.x < 64) {
+      const bool f = i0 + threadIdx.x < w.n_wg && w.fb_flags[i0 + threadIdx.x] != 0u;
+      const uint64_t bits = __builtin_amdgcn_ballot_w64(f);
+      if (threadIdx.x == 0) sbits = bits;
+    }
+    __syncthreads();
+    uint64_t bits = sbits;
+    while (bits) {
+      const int i = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      topk_rows16<NP, El, QM, TW>(a, w, smem, (i0 + i) * 16, true);
+    }
+    return;
+  }
+  const bool left = topk_rows16<NP, El, QM, TW>(a, w, smem, (int64_t)blockIdx.x * 16, false);
+  if (sizeof(El) == 4 && threadIdx.x == 0) w.fb_flags[blockIdx.x] = left ? 1u : 0u;
 }
 
 // one wave per row (mxa_topk_wave.hpp): waves of a 256-thread workgroup take rows

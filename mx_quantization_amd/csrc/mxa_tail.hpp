@@ -266,6 +266,11 @@ struct TailArgs {
   int64_t* idx_out;     // nullable: then idx16
   uint16_t* idx16;
   uint32_t* mask_out;   // nullable
+  // the standalone top-k (mxa_topk_ws): the values at the kept indices (nullable out_vals)
+  const void* vals;     // dtype dt, row stride ld
+  int64_t ld;
+  int dt;
+  void* out_vals;
 };
 
 // one lane per row; a workgroup of kTailWaves waves, each wave's 64 rows' prefixes in LDS
@@ -365,6 +370,7 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
     const int ix = (int)((uint32_t)A[p] & 0xFFu);
     if (a.idx_out) a.idx_out[row * k + p] = ix;
     else a.idx16[row * k + p] = (uint16_t)ix;
+    if (a.out_vals) store_dt(a.out_vals, row * k + p, load_dt(a.vals, row * a.ld + ix, a.dt), a.dt);
   }
   if (a.mask_out) {  // zeros.scatter_(-1, idx, 1) as bits
     for (int w = 0; w < a.ntw; ++w) {

@@ -146,8 +146,15 @@ def topk(vals: torch.Tensor, k: int, return_mask: bool = False):
     out = torch.empty(vals.shape[:-1] + (k,), dtype=vals.dtype, device=dev)
     mask = torch.empty(vals.shape[:-1] + ((n + 31) // 32,), dtype=torch.int32, device=dev) if return_mask else None
     if rows:
-        check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(),
-                             mask.data_ptr() if return_mask else None, dt, stream_ptr(dev)), "mxa_topk")
+        # the workspace path (rows of <= 256 values: the fused op's packed selection pass
+        # and one-lane tail); 0 bytes: mxa_topk alone
+        wsb = lib().mxa_topk_workspace_bytes(rows, n, k)
+        if wsb < 0:
+            raise ValueError(f"topk: invalid shape rows={rows} n={n} k={k}")
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        check(lib().mxa_topk_ws(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(),
+                                mask.data_ptr() if return_mask else None, dt, ws.data_ptr(), wsb,
+                                stream_ptr(dev)), "mxa_topk")
     return (out, idx, mask) if return_mask else (out, idx)
 
 

@@ -158,6 +158,10 @@ def test_hbm_traffic_never_averages_two_instantiations_of_a_stage():
     assert out["kernels"][dit]["write_bytes"] == 473145.0 * 1024
     assert out["kernels"][deit]["traffic_bytes"] == (2 * 10.0 + 143250.0) * 1024
     assert "select" not in out["stages"] and sorted(out["ambiguous"]["select"]) == sorted([deit, dit])
+    assert out["stages"]["finish"] == (2 * 100.0 + 200.0) * 1024
+    # a run with one instantiation per stage maps every stage
+    one = ht.combine(ht.per_kernel(rows[:14], "FETCH_SIZE"), ht.per_kernel(rows[:14], "WRITE_SIZE"))
+    assert one["stages"] == {"select": (2 * 10.0 + 143250.0) * 1024} and not one["ambiguous"]
 
 
 def test_hbm_traffic_select_stage_sums_its_kernels():
@@ -175,15 +179,11 @@ def test_hbm_traffic_select_stage_sums_its_kernels():
     out = ht.combine(ht.per_kernel(rows, "FETCH_SIZE"), ht.per_kernel(rows, "WRITE_SIZE"))
     assert out["stages"]["select"] == 3 * 111.0 * 1024
     assert out["stages"]["select_parts"]["select_tail"] == 3 * 10.0 * 1024
-    assert out["stages"]["finish"] == (2 * 100.0 + 200.0) * 1024
-    # a run with one instantiation per stage maps every stage
-    one = ht.combine(ht.per_kernel(rows[:14], "FETCH_SIZE"), ht.per_kernel(rows[:14], "WRITE_SIZE"))
-    assert one["stages"] == {"select": (2 * 10.0 + 143250.0) * 1024} and not one["ambiguous"]
 
 
 def test_bench_limiter_from_profiles(tmp_path):
     import bench
-    sel = "void mxa::select_q_kernel<256, 3, 2, 16, false>(mxa::Rows2Args)"
+    sel = "void mxa::select_kernel<256, 3, 2, unsigned int, 1, 64>(mxa::Rows2Args)"
     tj, pj = tmp_path / "t.json", tmp_path / "p.json"
     tj.write_text(json.dumps({"stages": {"select": 160e6}}))
     # 0.5 ms: HBM 160 MB -> 0.04 of peak; VALU 436 M instr x 2 cycles over 1024 SIMDs at 2.4 GHz -> 0.71
@@ -194,7 +194,7 @@ def test_bench_limiter_from_profiles(tmp_path):
     assert abs(lim["fracs"]["valu_issue"] - 436e6 * 2 / (1024 * 2.4e9 * 0.5e-3)) < 1e-9
     assert lim["lds_conflict_cycles_per_lds_instr"] == 0.5
     # two instantiations of the stage in the PMC file: no kernel is picked
-    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("false>", "true>"): {"SQ_INSTS_VALU": 1.0}}))
+    pj.write_text(json.dumps({sel: {"SQ_INSTS_VALU": 1.0}, sel.replace("1, 64>", "0, 0>"): {"SQ_INSTS_VALU": 1.0}}))
     _, lim = bench.profile_of({"pmc": str(pj)}, "select", 0.5, 320.0)
     assert "kernel" not in lim and lim["bound"] == "hbm"
 

@@ -91,8 +91,10 @@ def combine(fetch, write):
     for st, parts in STAGE_PARTS.items():  # whole-stage sums: one instantiation per part
         if any(p in ambiguous for p in parts) or not any(p in stages for p in parts):
             continue
-        stages[st + "_parts"] = {p: stages[p] for p in parts if p in stages}
-        stages[st] = sum(stages[p] for p in parts if p in stages)
+        got = {p: stages[p] for p in parts if p in stages}
+        if len(got) > 1:
+            stages[st + "_parts"] = got
+        stages[st] = sum(got.values())
     return {"kernels": kernels, "stages": stages, "ambiguous": ambiguous,
             "note": "traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes, gfx950 correction), "
                     "per launch, averaged over the dispatches of ONE kernel instantiation"}
