@@ -612,7 +612,10 @@ def test_qkv_projection_spread_paths(M, H):
     spreads 9 .. smax, or a head whose weight columns spread 10), fp64 block sums (wider,
     up to the 34-bit span they hold exactly).
     Rows scale alternate 32-channel blocks by 2^s; one head's q columns by 2^10, another's
-    k columns by 2^8 (the digit limit itself); H = 2 (D = 128) the widest head."""
+    k columns by 2^8 (the digit limit itself); H = 2 (D = 128) the widest head.  The first
+    32-token tile has every 32-channel block normalised to one exponent before its shift
+    (s <= 8), so its row spreads are the shifts themselves: the digit path for the head
+    groups whose weight columns spread <= 8; later tiles spread 9 .. 30."""
     B, N, C = 2, 70, 256
     D = C // H
     rng = np.random.default_rng(11 + H)
@@ -620,9 +623,12 @@ def test_qkv_projection_spread_paths(M, H):
     W = (rng.standard_normal((3 * C, C), dtype=np.float32) * np.float32(0.05)).astype(np.float32)
     bias = (rng.standard_normal(3 * C, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
     odd = (np.arange(C) // 32) % 2 == 1
+    blk = x[:, :32].reshape(B, 32, C // 32, 32)
+    e = np.floor(np.log2(np.abs(blk).max(-1, keepdims=True)))
+    x[:, :32] = (blk * np.float32(2.0) ** -e).reshape(B, 32, C).astype(np.float32)  # block max in [1, 2)
     shifts = [0, 3, 8, 9, 12, 20, 30]  # fp64 block sums are exact to a 34-bit span
     for t in range(N):
-        s = shifts[(t // 5) % len(shifts)]  # whole token blocks mostly share one spread
+        s = shifts[(t // 5) % 3] if t < 32 else shifts[(t // 5) % len(shifts)]  # first tile: s <= 8
         x[:, t, odd] *= np.float32(2.0 ** s)
     W[0 * C + 0 * D: 0 * C + 0 * D + D][:, odd] *= np.float32(2.0 ** 10)  # head 0's q columns
     hk = min(1, H - 1)
