@@ -6,12 +6,6 @@
 #include "mxa_finish16.hpp"
 #include "mxa_launch.hpp"
 
-// 1: the finishing kernel on 16-row tiles for k <= 64 (mxa_finish16.hpp; default); 0: the
-// 32-row kernel for every k (A/B builds)
-#ifndef MXA_FIN16
-#define MXA_FIN16 1
-#endif
-
 namespace mxa {
 
 // ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
@@ -197,7 +191,7 @@ static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool p
   // The proj's MX input codes (XO) stay on the 32-row kernel: its 32 x 32 output blocks are
   // whole MX blocks of the output rows (measured: 0.264 ms at DeiT-base against 0.308 ms
   // for 16-row tiles, whose 16 x 32 blocks take twice the transposes and syncs per row).
-  if (MXA_FIN16 && ra.k_top <= 64 && !ra.xo_codes) {
+  if (ra.k_top <= 64 && !ra.xo_codes) {
     if (plan) {
       int w, r;
       return finish16_plan(ra, BH, 2, &w, &r);

@@ -33,9 +33,7 @@
 namespace mxa {
 
 constexpr int kFin16 = 16;  // query rows per MFMA tile (one wave)
-#ifndef MXA_FIN16_OCC  // waves per SIMD the register allocation aims at
-#define MXA_FIN16_OCC 4
-#endif
+constexpr int kFin16Occ = 4;  // waves per SIMD the register allocation aims at
 // (the MFMA B operands, V^T codes, come straight from memory: staged in LDS with the K
 // table they measured 0.214 ms at 3 waves per SIMD against 0.200 ms at 4, DeiT-base)
 
@@ -66,7 +64,7 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
 }
 
 template <int NB, int KS, int LPR, bool XDT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && KS <= 12 ? MXA_FIN16_OCC : (NB * KS <= 64 ? 3 : 2), 8))) void finish16_kernel(Rows2Args a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && KS <= 12 ? kFin16Occ : (NB * KS <= 64 ? 3 : 2), 8))) void finish16_kernel(Rows2Args a) {
   static_assert(LPR == 4 || LPR == 16, "four or sixteen lanes per query row");
   const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

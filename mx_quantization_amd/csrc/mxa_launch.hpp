@@ -10,9 +10,9 @@ inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr
 
 // selection kernel (mxa_sel.hip); plan: only check the LDS budget, launch nothing
 int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);
-#ifndef MXA_TAIL_PREF
-#define MXA_TAIL_PREF 64  // the one-lane tail's prefix when k allows (32 or 64)
-#endif
+// the one-lane tail's prefix (measured: a 32-position prefix for k <= 30 is no faster -- the
+// selection kernel then runs one more lockstep step per row)
+constexpr int kTailPref = 64;
 // the selection's packed pass: rows of <= 256 keys, the approximators whose scores pack
 // (sums of a few small integers times powers of two), no bias (a bias of -10000 next to
 // small scores needs the key's low byte: PixArt's masked cross-attention would fall back
@@ -25,7 +25,7 @@ inline bool sel_packs(int mode, int T, bool bias) {
 // (k - 1 <= 32: the final stable rank of [0, k-1) in at most 32 registers per lane)
 inline int sel_tail_width(int mode, int T, int k, bool bias) {
   if (!sel_packs(mode, T, bias) || k <= 0 || k > 33 || (int64_t)k * 64 <= T) return 0;
-  if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
+  if (k + 2 <= kTailPref) return kTailPref;
   return k + 2 <= 64 ? 64 : 0;
 }
 
@@ -50,10 +50,7 @@ inline int launch_select_mode(const Rows2Args& ra, int mode, int BH, hipStream_t
 // share of T (above the 16-row gather kernel's k <= 64), T <= 256 (the scores of a row in
 // registers); not with the proj Linear's MX input codes (xo).  It reads the selection's
 // prune-mask words (the caller's mask_out, else a workspace copy), not the kept indices.
-#ifndef MXA_FQ_MINK
-#define MXA_FQ_MINK 65
-#endif
-inline bool finish_qk_wanted(int k, int T, int nbd, bool xo) { return k >= MXA_FQ_MINK && T <= 256 && nbd <= 4 && !xo; }
+inline bool finish_qk_wanted(int k, int T, int nbd, bool xo) { return k >= 65 && T <= 256 && nbd <= 4 && !xo; }
 // its launches (mxa_fin_qk.hip): float32 inputs and scores (x0), float16 / bfloat16 (x1)
 int launch_finish_qk_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
 int launch_finish_qk_x1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);

@@ -138,7 +138,7 @@ static int launch_topk_grp(const GrpTopkArgs& ga, const TopkWs& w, unsigned grid
 // pass over the rows it leaves
 static int topk_ws_tw(int n, int k) {
   if (k <= 0 || k > 33 || (int64_t)k * 64 <= n) return 0;
-  if (k + 2 <= MXA_TAIL_PREF) return MXA_TAIL_PREF;
+  if (k + 2 <= kTailPref) return kTailPref;
   return k + 2 <= 64 ? 64 : 0;
 }
 static bool topk_ws_packs(int n, int k) { return n <= 256 && k > 0; }

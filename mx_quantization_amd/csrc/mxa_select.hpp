@@ -29,30 +29,27 @@
 
 namespace mxa {
 
-#ifndef MXA_SEL_ROWS  // tools builds vary these (build_native defines)
-#define MXA_SEL_ROWS 32
-#endif
-#ifndef MXA_SEL_OCC
-#define MXA_SEL_OCC 4
-#endif
-#ifndef MXA_SEL_SHORT_T
-#define MXA_SEL_SHORT_T 224
-#endif
-#ifndef MXA_SELP_OCC
-#define MXA_SELP_OCC 5  // waves per SIMD the packed pass is compiled for
-#endif
-constexpr int kSelRows = MXA_SEL_ROWS;  // query rows per workgroup (a multiple of 4 * waves)
+constexpr int kSelRows = 32;   // query rows per workgroup (a multiple of 4 * waves)
+constexpr int kSelOcc = 4;     // waves per SIMD the 64-bit pass is compiled for (rows <= 256 keys)
+constexpr int kSelPOcc = 5;    // ... and the packed pass
+constexpr int kSelShortT = 224;
 // waves per workgroup: 2 for rows of <= 224 keys on a large grid (DeiT-base: 0.97 ->
 // 0.93 ms), else 4 (DiT: 1.44 vs 1.56 ms with 2; PixArt's 128 heads: 0.069 vs 0.10 ms)
 // -- measured, tools/bench_cmp.sh
 inline int sel_waves_for(int T, int64_t BH, int N) {
-  return T <= MXA_SEL_SHORT_T && BH * ((N + kSelRows - 1) / kSelRows) >= 8192 ? 2 : 4;
+  return T <= kSelShortT && BH * ((N + kSelRows - 1) / kSelRows) >= 8192 ? 2 : 4;
 }
 
 // LDS layout of the score tables (then the per-row top-k areas)
 struct SelLds {
-  size_t cd, ex, sg, z, cs, rows;
+  size_t cd, ex, sg, z, cs, kf, rows;
 };
+// ex_pred's key exponents go to LDS as int32 for nbd <= 2 (raw int16 values sign-extended:
+// no extraction in the key loop; for nbd >= 3 int16, which keeps DiT's workgroups per CU),
+// with 16 flag words kf: bit i of kf[g] = key g + 16 i has a
+// block exponent outside [kExpFastLo, kExpFastHi] (or NaN), i.e. its score may need the
+// exact slow path (sel_scores)
+constexpr int kExpFastLo = -50, kExpFastHi = 61;
 __host__ __device__ inline SelLds sel_lds(int mode, int T, int D, int kst, int nbd) {
   SelLds L;
   size_t o = 0;
@@ -61,13 +58,15 @@ __host__ __device__ inline SelLds sel_lds(int mode, int T, int D, int kst, int n
   L.cd = o;
   if (codes) o += al((size_t)T * kst);
   L.ex = o;
-  if (mode != kModeElsa) o += al((size_t)T * nbd * 2);
+  if (mode != kModeElsa) o += al((size_t)T * nbd * (mode == kModeExSign && nbd <= 2 ? 4 : 2));
   L.sg = o;
   if (mode == kModeExSign || mode == kModeElsa) o += al((size_t)T * nbd * 4);
   L.z = o;
   if (mode == kModeTrueEx) o += al((size_t)T * kst);
   L.cs = o;
   if (mode == kModeElsa) o += al((size_t)(D + 1) * 4);
+  L.kf = o;
+  if (mode == kModeExSign) o += 16 * 4;
   L.rows = o;
   return L;
 }
@@ -90,15 +89,15 @@ __device__ __forceinline__ int dot32(const uint4& a0, const uint4& a1, const uin
 // the sum shifted to the smallest exponent is an exact int32, so one conversion (round
 // to nearest even) and an exact scaling give the correctly rounded float; otherwise
 // (and for NaN blocks) the exact fp64 sum.  Both equal fl32 of the exact sum.
-template <int NBD>
-__device__ __forceinline__ float expred_score(const uint32_t* sq, const int* eq, const int16_t* kex, const uint32_t* ksg,
+template <int NBD, typename KE>
+__device__ __forceinline__ float expred_score(const uint32_t* sq, const int* eq, const KE* kex, const uint32_t* ksg,
                                               int D) {
   int m[NBD], e[NBD];
   bool nan = false;
   int emin = 1 << 20, emax = -(1 << 20);
 #pragma unroll
   for (int b = 0; b < NBD; ++b) {
-    const int ek = exp_from16(kex[b]);
+    const int ek = exp_from16((int16_t)kex[b]);
     nan = nan || ek == kExpNaN || eq[b] == kExpNaN;
     e[b] = eq[b] + ek;
     m[b] = min(32, D - 32 * b) - 2 * (int)__popc(sq[b] ^ ksg[b]);
@@ -218,7 +217,9 @@ __device__ __forceinline__ float elsa_cos_entry(int D, int h) {
 // ---- the head's score tables in LDS (sel_lds) -------------------------------------
 struct SelTabs {
   int8_t* tcd;    // key codes
-  int16_t* tex;   // key exponents
+  int16_t* tex;   // key exponents (ex_pred: tex32)
+  int* tex32;
+  uint32_t* kf;   // ex_pred: the keys outside the fast path's exponent range (SelLds)
   uint32_t* tsg;  // sign / hash words
   int8_t* tz;     // true_ex zero indicators
   float* tcs;     // ELSA cosine table
@@ -232,7 +233,13 @@ __device__ __forceinline__ SelTabs sel_stage(const Rows2Args& a, unsigned char* 
   t.tsg = reinterpret_cast<uint32_t*>(smem + L.sg);
   t.tz = reinterpret_cast<int8_t*>(smem + L.z);
   t.tcs = reinterpret_cast<float*>(smem + L.cs);
+  t.tex32 = reinterpret_cast<int*>(smem + L.ex);
+  t.kf = reinterpret_cast<uint32_t*>(smem + L.kf);
   const int T = a.T, D = a.D, nbd = a.nbd, kst = a.kst;
+  if (MODE == kModeExSign && nbd <= 2) {  // (the range flags serve the nbd <= 2 key loop)
+    if (threadIdx.x < 16) t.kf[threadIdx.x] = 0u;
+    __syncthreads();
+  }
   const int64_t kb = (int64_t)bh * T;
   if constexpr (MODE == kModeTrue || kOp || MODE == kModeTrueEx) {
     const int8_t* src = MODE == kModeTrue ? a.kc : a.kop;
@@ -249,7 +256,20 @@ __device__ __forceinline__ SelTabs sel_stage(const Rows2Args& a, unsigned char* 
   {
     const int16_t* esrc = MODE == kModeTrue ? a.ksT : a.ksA;
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) {
-      if (MODE != kModeElsa) t.tex[i] = esrc[kb * nbd + i];
+      if (MODE == kModeExSign) {
+        const int ek = esrc[kb * nbd + i];  // raw (NaN: INT16_MIN, outside the range)
+        if (nbd <= 2) {
+          t.tex32[i] = ek;
+          if (ek < kExpFastLo || ek > kExpFastHi) {
+            const int j = i / nbd;
+            atomicOr(t.kf + (j & 15), 1u << (j >> 4));
+          }
+        } else {
+          t.tex[i] = (int16_t)ek;
+        }
+      } else if (MODE != kModeElsa) {
+        t.tex[i] = esrc[kb * nbd + i];
+      }
       if (MODE == kModeExSign || MODE == kModeElsa) t.tsg[i] = a.ksg[kb * nbd + i];
     }
     if (MODE == kModeElsa)
@@ -260,8 +280,9 @@ __device__ __forceinline__ SelTabs sel_stage(const Rows2Args& a, unsigned char* 
 }
 
 // ---- the approximate (or true) scores of query row r: keys j0, j0 + js, ... -------------
-// sink(j, v, key): v the score as the caller ranks it (score dtype, + bias), key its order
-// key.  pred_out / true_out are written here.
+// sink(j, v, key, fast): v the score as the caller ranks it (score dtype, + bias), key its order
+// key, fast (std::true_type) when v came from the fast ex_pred loop (finite, never -0)
+// pred_out / true_out are written here.
 template <int MODE, typename Sink>
 __device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t, int bh, int r, int j0, int js,
                                            Sink&& sink) {
@@ -280,7 +301,7 @@ __device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t,
     } else if (a.pred_out) {
       a.pred_out[grow * T + j] = v;
     }
-    sink(j, v, order_key(v));
+    sink(j, v, order_key(v), std::false_type{});
   };
   if constexpr (MODE == kModeExSign) {
     // pred = sum_b 2^(eq_b + ek_b) (n_b - 2 popc(sq_b ^ sk_b))   (exact)
@@ -293,50 +314,105 @@ __device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t,
     }
     auto keys = [&](auto nbd_c) {  // the key loop for a compile-time block count
       constexpr int NBD = decltype(nbd_c)::value;
-      if (brow >= 0 || a.s_dt != kF32) {
-        for (int j = j0; j < T; j += js) emit(j, expred_score<NBD>(sq, eq, t.tex + j * NBD, t.tsg + j * NBD, D));
+      if (brow >= 0 || a.s_dt != kF32 || js != 16) {
+        if constexpr (NBD <= 2)
+          for (int j = j0; j < T; j += js) emit(j, expred_score<NBD>(sq, eq, t.tex32 + j * NBD, t.tsg + j * NBD, D));
+        else
+          for (int j = j0; j < T; j += js) emit(j, expred_score<NBD>(sq, eq, t.tex + j * NBD, t.tsg + j * NBD, D));
         return;
       }
-      // no bias: the raw int16 exponents (NaN = INT16_MIN) go straight into the
-      // fast-path test -- a NaN block drives the smallest exponent below -100 --
-      // and a fast-path value (finite, never -0) takes the three-instruction key
-      int eqr[NBD], nbk[NBD];
-#pragma unroll
-      for (int b = 0; b < NBD; ++b) {
-        eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
-        nbk[b] = min(32, D - 32 * b);
-      }
-      float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
-      for (int j = j0; j < T; j += js) {
-        const int16_t* kex = t.tex + j * NBD;
-        const uint32_t* ksg = t.tsg + j * NBD;
-        int e[NBD], m[NBD];
+      if constexpr (NBD >= 3) {
+        // the bias-free key loop on raw int16 exponents (NaN = INT16_MIN drives the smallest
+        // exponent below -100): a fast-path value (finite, never -0) takes the
+        // three-instruction key.  (The branch-free loop below measured slower at DiT's three
+        // blocks: its extra live values spill.)
+        int eqr[NBD], nbk[NBD];
 #pragma unroll
         for (int b = 0; b < NBD; ++b) {
-          e[b] = eqr[b] + (int)kex[b];
-          m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
+          eqr[b] = eq[b] == kExpNaN ? (int)kExpNaN16 : eq[b];
+          nbk[b] = min(32, D - 32 * b);
         }
-        int emin = e[0], emax = e[0];
+        float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
+        for (int j = j0; j < T; j += js) {
+          const int16_t* kex = t.tex + j * NBD;
+          const uint32_t* ksg = t.tsg + j * NBD;
+          int e[NBD], m[NBD];
 #pragma unroll
-        for (int b = 1; b < NBD; ++b) {
-          emin = min(emin, e[b]);
-          emax = max(emax, e[b]);
-        }
-        float v;
-        uint32_t key;
-        if (emax - emin <= 23 && emin >= -100) {
-          int sum = 0;
+          for (int b = 0; b < NBD; ++b) {
+            e[b] = eqr[b] + (int)kex[b];
+            m[b] = nbk[b] - 2 * (int)__popc(sq[b] ^ ksg[b]);
+          }
+          int emin = e[0], emax = e[0];
 #pragma unroll
-          for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
-          v = ldexpf((float)sum, emin);
-          const uint32_t u = __float_as_uint(v);
-          key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
-        } else {
-          v = expred_score<NBD>(sq, eq, kex, ksg, D);
-          key = order_key(v);
+          for (int b = 1; b < NBD; ++b) {
+            emin = min(emin, e[b]);
+            emax = max(emax, e[b]);
+          }
+          float v;
+          uint32_t key;
+          if (emax - emin <= 23 && emin >= -100) {
+            int sum = 0;
+#pragma unroll
+            for (int b = 0; b < NBD; ++b) sum += m[b] << (e[b] - emin);
+            v = ldexpf((float)sum, emin);
+            const uint32_t u = __float_as_uint(v);
+            key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
+          } else {
+            v = expred_score<NBD>(sq, eq, kex, ksg, D);
+            key = order_key(v);
+          }
+          if (prow) prow[j] = v;
+          sink(j, v, key, std::false_type{});
         }
-        if (prow) prow[j] = v;
-        sink(j, v, key);
+        return;
+      }
+      // No bias, float32 scores: every lane runs the same ceil(T / 16) keys (the last trip
+      // peeled: keys >= T are dropped), with no branch in the loop.  When every block
+      // exponent of the row and of the key lies in [kExpFastLo, kExpFastHi], the block
+      // terms m_b 2^(eq_b + ek_b) are exact floats (|m_b| <= 32, 2^-100 <= 2^e <= 2^122):
+      // v = x0 + x1, one IEEE addition of two exact terms = fl32(exact sum) (NBD <= 2).
+      // Keys outside (range flags kf, a NaN block) are redone afterwards by
+      // the exact expred_score, under a wave-uniform branch.  A fast value is finite and
+      // never -0, so its order key takes two instructions and its packing test is the low
+      // byte of its bits.
+      int nbk[NBD];
+      bool row_fast = true;
+#pragma unroll
+      for (int b = 0; b < NBD; ++b) {
+        nbk[b] = min(32, D - 32 * b);
+        row_fast = row_fast && eq[b] >= kExpFastLo && eq[b] <= kExpFastHi;  // (NaN: kExpNaN)
+      }
+      float* prow = a.pred_out ? a.pred_out + grow * T : nullptr;
+      const int nt = (T + 15) >> 4;
+      uint32_t redo = row_fast ? t.kf[j0 & 15] : lowbits(nt);  // per trip i: key j0 + 16 i
+      auto one = [&](int i, auto last_c) {
+        constexpr bool LAST = decltype(last_c)::value;
+        const int j = j0 + 16 * i;
+        const int* kex = t.tex32 + j * NBD;
+        const uint32_t* ksg = t.tsg + j * NBD;
+        float v = ldexpf((float)(nbk[0] - 2 * (int)__popc(sq[0] ^ ksg[0])), eq[0] + kex[0]);
+        if constexpr (NBD == 2) v += ldexpf((float)(nbk[1] - 2 * (int)__popc(sq[1] ^ ksg[1])), eq[1] + kex[1]);
+        const uint32_t u = __float_as_uint(v);
+        const uint32_t key = u ^ ((uint32_t)((int)u >> 31) | 0x80000000u);
+        if (!LAST || j < T) {
+          if (prow) prow[j] = v;
+          sink(j, v, key, std::true_type{});
+        }
+      };
+#pragma unroll 1
+      for (int i = 0; i < nt - 1; ++i) one(i, std::false_type{});
+      one(nt - 1, std::true_type{});
+      if (__builtin_amdgcn_ballot_w64(redo != 0u) != 0) {  // rare: the exact path for those keys
+        while (redo) {
+          const int i = __ffs((int)redo) - 1;
+          redo &= redo - 1u;
+          const int j = j0 + 16 * i;
+          if (j < T) {
+            const float v = expred_score<NBD>(sq, eq, t.tex32 + j * NBD, t.tsg + j * NBD, D);
+            if (prow) prow[j] = v;
+            sink(j, v, order_key(v), std::false_type{});
+          }
+        }
       }
     };
     switch (nbd) {
@@ -430,7 +506,7 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
   bool valid = r < r_end;
   const int64_t grow = (int64_t)bh * a.N + (valid ? r : rq);
   if (!kPacked && a.fb_only && valid) valid = kept_get(a, grow * k) < 0;
-  uint32_t bad = 0u;
+  uint32_t bad = 0u, badf = 0u;
 #ifdef MXA_SEL_SKIP
   if (valid && !((MXA_SEL_SKIP) & 2))
 #else
@@ -438,13 +514,15 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
 #endif
   {
     if constexpr (kPacked)
-      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float v, uint32_t key) {
-        bad |= q_bad_bits(v);
+      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float v, uint32_t key, auto fast_c) {
+        if constexpr (decltype(fast_c)::value) badf |= __float_as_uint(v);  // finite: the low byte
+        else bad |= q_bad_bits(v);
         g.A[j] = qelem(key, (uint32_t)j);
       });
     else
-      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float, uint32_t key) { g.A[j] = pack_ki(key, (uint32_t)j); });
+      sel_scores<MODE>(a, t, bh, r, gl, 16, [&](int j, float, uint32_t key, auto) { g.A[j] = pack_ki(key, (uint32_t)j); });
   }
+  bad |= badf & 0xFFu;
 #ifdef MXA_SEL_SKIP  // tools-only phase timing (build_native defines): 2 = scores replaced by hashed keys
   if ((MXA_SEL_SKIP) & 2)
     for (int j = gl; j < T; j += 16) {
@@ -462,11 +540,11 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
     }
   }
   wave_lds_sync();
+  GrpHand hand{0u, false};
 #ifdef MXA_SEL_SKIP  // 1 = no top-k
   if (!((MXA_SEL_SKIP) & 1))
 #endif
-  GrpHand hand{0u, false};
-  grp_topk<NP, El, QM, TW>(g, T, k, valid, gl, &hand);
+    grp_topk<NP, El, QM, TW>(g, T, k, valid, gl, &hand);
   if (TW > 0 && hand.on) {  // the row's state and prefix to the tail kernel
     uint32_t* rec = a.tail_rec + grow * tail_rec_words(TW);
     if (gl == 0) {
@@ -519,7 +597,7 @@ __device__ __forceinline__ bool select_item(const Rows2Args& a, unsigned char* s
 // flags, taking the flagged items one after another (a call without such rows costs a
 // small grid that exits at once).
 template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
-__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? MXA_SELP_OCC : NP <= 256 ? MXA_SEL_OCC : 2, 8))) void select_kernel(Rows2Args a) {
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? kSelPOcc : NP <= 256 ? kSelOcc : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (sizeof(El) == 8 && a.fb_only) {
     __shared__ uint64_t sbits;

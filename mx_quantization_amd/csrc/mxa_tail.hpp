@@ -359,6 +359,8 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
   if (__builtin_amdgcn_ballot_w64(ph == 3 && m >= 2) != 0) {  // (m <= 32: sel_tail_width)
     if (m <= 16) {
       if (ph == 3) t_rank<16>(A, m);
+    } else if (m <= 20) {  // DeiT's k = 20
+      if (ph == 3) t_rank<20>(A, m);
     } else if (m <= 24) {
       if (ph == 3) t_rank<24>(A, m);
     } else {
@@ -366,22 +368,18 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
     }
   }
   if (!pend) return;
+  // the kept indices, and the prune-mask words (zeros.scatter_(-1, idx, 1) as bits) set in
+  // the lane's own stack slots (free now; ntw <= 8 < kTailStk) by LDS ORs
+  const int ntw = a.mask_out ? a.ntw : 0;
+  for (int w = 0; w < ntw; ++w) stk[w] = 0u;
   for (int p = 0; p < k; ++p) {
-    const int ix = (int)((uint32_t)A[p] & 0xFFu);
-    if (a.idx_out) a.idx_out[row * k + p] = ix;
+    const uint32_t ix = (uint32_t)A[p] & 0xFFu;
+    if (a.idx_out) a.idx_out[row * k + p] = (int64_t)ix;
     else a.idx16[row * k + p] = (uint16_t)ix;
     if (a.out_vals) store_dt(a.out_vals, row * k + p, load_dt(a.vals, row * a.ld + ix, a.dt), a.dt);
+    if (ntw) __hip_atomic_fetch_or(stk[(int)(ix >> 5)].p, 1u << (ix & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
-  if (a.mask_out) {  // zeros.scatter_(-1, idx, 1) as bits
-    for (int w = 0; w < a.ntw; ++w) {
-      uint32_t word = 0u;
-      for (int p = 0; p < k; ++p) {
-        const uint32_t ix = (uint32_t)A[p] & 0xFFu;
-        word |= (ix >> 5) == (uint32_t)w ? 1u << (ix & 31) : 0u;
-      }
-      a.mask_out[row * a.ntw + w] = word;
-    }
-  }
+  for (int w = 0; w < ntw; ++w) a.mask_out[row * ntw + w] = (uint32_t)stk[w];
 }
 
 __host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * (TW + kTailStk) * 4; }

@@ -437,7 +437,8 @@ def test_expred_paths_vs_oracle(M, D, N, T, k):
 @pytest.mark.parametrize("k", [20, 100])
 def test_expred_special_rows(M, k):
     """Zero K rows (exponent -126 blocks), a wide exponent spread, NaN / Inf
-    inputs, rows whose true scores overflow, all-zero query rows; k on the gather
+    inputs, rows whose true scores overflow, all-zero query rows, block exponents around
+    the bounds of the ex_pred key loop's fast range; k on the gather
     finishing kernel (20) and on the MFMA one (100: every key's exact epilogue, its fp64
     and NaN branches)."""
     rng = np.random.default_rng(5)
@@ -453,6 +454,11 @@ def test_expred_special_rows(M, k):
     q[1, 1, 17, :] *= np.float32(2.0 ** 100)    # true scores overflow for this row
     kk[1, 1, :, :] *= np.float32(2.0 ** 30)
     q[1, 2, :4, :] = 0.0                        # zero query rows (all preds tie)
+    # block exponents across the ex_pred key loop's fast range [-50, 61] (mxa_select.hpp
+    # kExpFastLo / Hi): keys at 2^59..2^63, query rows at 2^-49..-53, one key's blocks split
+    kk[1, 3, :40, :] *= (np.float32(2.0) ** np.arange(59, 64, dtype=np.float32).repeat(8))[:, None]
+    q[1, 3, 40:80, :] *= (np.float32(2.0) ** -np.arange(49, 54, dtype=np.float32).repeat(8))[:, None]
+    kk[1, 3, 100, 32:] *= np.float32(2.0 ** -60)
     outs = _attn_all_paths(M, q, kk, v, 0.125, k_top=k)
     r = O.attention(q, kk, v, 0.125, k_top=k)
     for got, name in zip(outs, PATHS):
