@@ -31,6 +31,18 @@ __device__ __forceinline__ uint32_t q_bad_bits(float v) {
   const uint32_t u = __float_as_uint(v);
   return (u & 0x7FFFFFFFu) > 0x7F800000u ? 0u : (u & 0xFFu);
 }
+// nonzero for the values a packed element does not give back bit for bit (q_value): NaN
+// (payload) and -0 (its order key is +0's)
+__device__ __forceinline__ uint32_t q_val_bad(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (uint32_t)((u & 0x7FFFFFFFu) > 0x7F800000u || u == 0x80000000u);
+}
+// the value of a packed element whose value packs (q_bad_bits == 0) and is neither NaN nor
+// -0: the order key's low byte is 0x00 (positive) or 0xFF (negative), then order_key undone
+__device__ __forceinline__ float q_value(uint32_t e) {
+  const uint32_t key = (e & 0x80000000u) ? (e & 0xFFFFFF00u) : (e | 0xFFu);
+  return __uint_as_float((key & 0x80000000u) ? (key & 0x7FFFFFFFu) : ~key);
+}
 
 __device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
 

@@ -665,6 +665,7 @@ __device__ __forceinline__ bool topk_rows16(const GrpTopkArgs& a, const TopkWs& 
       const float v = load_dt(a.vals, src + j, a.dt);
       if constexpr (kPacked) {
         bad |= q_bad_bits(v);
+        if (a.out_vals) bad |= q_val_bad(v);  // the tail rebuilds the values from the elements
         g.A[j] = qelem(order_key(v), (uint32_t)j);
       } else {
         g.A[j] = pack_ki(order_key(v), (uint32_t)j);

@@ -276,6 +276,7 @@ struct TailArgs {
 // one lane per row; a workgroup of kTailWaves waves, each wave's 64 rows' prefixes in LDS
 constexpr int kTailWaves = 1;
 constexpr int kTailStk = 12;  // introsort stack entries (depth limit 2 lg(32) + 1 = 11)
+constexpr int kTailMaxK = 33;  // k handed to the tail (k - 1 <= 32: the final rank's width)
 template <int TW>
 __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -368,18 +369,26 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
     }
   }
   if (!pend) return;
-  // the kept indices, and the prune-mask words (zeros.scatter_(-1, idx, 1) as bits) set in
-  // the lane's own stack slots (free now; ntw <= 8 < kTailStk) by LDS ORs
+  // the kept indices (k <= kTailMaxK: sel_tail_width / topk_ws_tw), and the prune-mask words
+  // (zeros.scatter_(-1, idx, 1) as bits) set in the lane's own stack slots (free now; ntw <= 8
+  // < kTailStk) by LDS ORs; the standalone top-k's values at the kept indices come back from
+  // the packed elements themselves (q_value: no gather from the input rows)
+  uint32_t ix[kTailMaxK];
+#pragma unroll
+  for (int p = 0; p < kTailMaxK; ++p) ix[p] = p < k ? (uint32_t)A[p] & 0xFFu : 0u;
   const int ntw = a.mask_out ? a.ntw : 0;
   for (int w = 0; w < ntw; ++w) stk[w] = 0u;
-  for (int p = 0; p < k; ++p) {
-    const uint32_t ix = (uint32_t)A[p] & 0xFFu;
-    if (a.idx_out) a.idx_out[row * k + p] = (int64_t)ix;
-    else a.idx16[row * k + p] = (uint16_t)ix;
-    if (a.out_vals) store_dt(a.out_vals, row * k + p, load_dt(a.vals, row * a.ld + ix, a.dt), a.dt);
-    if (ntw) __hip_atomic_fetch_or(stk[(int)(ix >> 5)].p, 1u << (ix & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#pragma unroll
+  for (int p = 0; p < kTailMaxK; ++p) {
+    if (p < k) {
+      if (a.idx_out) a.idx_out[row * k + p] = (int64_t)ix[p];
+      else a.idx16[row * k + p] = (uint16_t)ix[p];
+      if (ntw) __hip_atomic_fetch_or(stk[(int)(ix[p] >> 5)].p, 1u << (ix[p] & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
   }
   for (int w = 0; w < ntw; ++w) a.mask_out[row * ntw + w] = (uint32_t)stk[w];
+  if (a.out_vals)  // (the packed pass sent no row with a NaN or -0 value: q_val_bad)
+    for (int p = 0; p < k; ++p) store_dt(a.out_vals, row * k + p, q_value((uint32_t)A[p]), a.dt);
 }
 
 __host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * (TW + kTailStk) * 4; }
