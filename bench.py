@@ -25,8 +25,9 @@ Besides the contract fields the JSON line carries
                 mfma:    Ops_gemm (dense QK^T + PV) over the finishing kernel's time
   cpu_baseline  the CPU oracle (oracle/, test infrastructure) on the host's cores
   parity        top-k index bit-match and output error of a sample of images per rank
-  secondary     the DiT-XL/2 line (the metric names both models) when --config deit_base, and
-                the qkv-Linear-fused line (mxa_qkv_attention) of the config
+  secondary     the DiT-XL/2 line (the metric names both models) when --config deit_base, the
+                qkv-Linear-fused lines (mxa_qkv_attention, + the proj Linear), the dense branch
+                (top_k=False) at the config's shape, and the drop-in modules' line
 """
 from __future__ import annotations
 
@@ -358,6 +359,7 @@ def run_config(c, images, steps, warmup, device, world, prof=None):
         lambda: N.check(N.lib().mxa_attention_timed(ctypes.byref(p), stream, steps, stage_ms), "mxa_attention_timed"),
         world, torch.cuda.synchronize, device)
     path = N.PATH_NAMES.get(N.lib().mxa_attention_path(ctypes.byref(p)), "?")
+    fin = fin_engines(p)
     stages = {name: float(stage_ms[slot]) for name, slot in zip(STAGES, STAGE_SLOTS)}
     cb = dict(c, B=B)
     by = stage_bytes(cb, path)
@@ -376,20 +378,75 @@ def run_config(c, images, steps, warmup, device, world, prof=None):
         "qa_pass": {"what": "SURVEY §8d Bytes_qa over the prep (Q, K, V) + selection kernels",
                     "bytes": bytes_qa(cb), "ms": qa_ms, "achieved": qa_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": qa_gbs / HBM_PEAK_GBS},
-        "mfma": {"what": "SURVEY §8d Ops_gemm (dense QK^T + PV int8 ops) over the finishing kernel's time; "
-                         "that kernel runs P.V on int8 MFMA (one per 32-key MX block and 16 / 32 output "
-                         "columns of a 16- / 32-row P tile) and the kept keys' QK^T with v_dot4, so this "
-                         "is the dense-equivalent rate",
+        "mfma": {"what": "SURVEY §8d Ops_gemm (dense QK^T + PV int8 ops) over the finishing kernel's time "
+                         "(the dense-equivalent rate; `engine` names the kernel the library launched and the "
+                         "units its two contractions run on, from mxa_attention_finish_kernel)",
                  "ops": ops_gemm(cb), "ms": stages["finish"], "achieved": mf_tops, "peak": I8_PEAK_TOPS,
-                 "unit": "TOPS", "frac": mf_tops / I8_PEAK_TOPS,
-                 # mxa_fin.hip launch_finish: 16-row tiles for k <= 64, else 32-row tiles
-                 "engine": ("P.V: v_mfma_i32_16x16x32_i8" if cb["k"] <= 64 else "P.V: v_mfma_i32_32x32x32_i8")
-                           + "; kept-key QK^T: v_dot4"},
+                 "unit": "TOPS", "frac": mf_tops / I8_PEAK_TOPS, "engine": fin},
     }
     e2e = {"fused_min_bytes": fused_min_bytes(cb),
            "achieved_GBs": fused_min_bytes(cb) / (sum(stages.values()) * 1e-3) / 1e9}
     e2e["frac"] = e2e["achieved_GBs"] / HBM_PEAK_GBS
     return elapsed, stages, roof, e2e, out, idx
+
+
+def fin_engines(p):
+    """The finishing kernel mxa_attention(p) launches and the engines of its QK^T and P.V
+    (include/mxa.h mxa_attention_finish_kernel: the library's own dispatch decision)."""
+    from mx_quantization_amd import _native as N
+    kind = N.lib().mxa_attention_finish_kernel(ctypes.byref(p))
+    name, qk, pv = N.FIN_KERNELS.get(kind, ("?", "?", "?"))
+    return {"kernel": name, "qk": qk, "pv": pv, "code": kind}
+
+
+def run_dense(c, images, steps, warmup, device, world):
+    """The dense branch (top_k=False: DeiT block 11, deit main.py:149-152; DiT's last block,
+    models.py:218-225) at the config's shape: attn = softmax(true scores) over every key, then
+    MX(P) @ MX(V).  Returns (elapsed, stage_ms, extra)."""
+    import torch
+    import mx_quantization_amd as M
+    from mx_quantization_amd import _native as N
+    t = lambda a: None if a is None else torch.from_numpy(a).to(device)
+    q, k, v, bias = (t(a) for a in make_inputs(c, images))
+    out = torch.empty_like(q)
+    for _ in range(max(warmup, 1)):
+        out, _ = M.mx_topk_attention(q, k, v, c["scale"], top_k=False, bias=bias, flush_subnormals=c["bias"], out=out)
+    torch.cuda.synchronize()
+    B = len(images)
+    p = N.AttnParams()
+    p.q, p.k, p.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+    p.q_strides[:], p.k_strides[:], p.v_strides[:] = q.stride()[:3], k.stride()[:3], v.stride()[:3]
+    p.B, p.H, p.N, p.T, p.D = B, c["H"], c["N"], c["T"], c["D"]
+    p.k_top, p.scale = 0, float(np.float32(c["scale"]))
+    p.pred_mode, p.top_k, p.approx = N.PRED_MODES[c["mode"]], 0, 1
+    p.flush_subnormals, p.bfloat = int(c["bias"]), 0
+    if bias is not None:
+        b4 = bias.expand(B, c["H"], c["N"], c["T"])
+        p.bias, p.bias_strides[:] = b4.data_ptr(), b4.stride()
+    p.out, p.out_strides[:] = out.data_ptr(), out.stride()[:3]
+    from mx_quantization_amd.ops import _workspace
+    ws = _workspace(device, N.lib().mxa_attention_workspace_bytes(ctypes.byref(p)))
+    p.workspace, p.workspace_bytes = ws.data_ptr(), ws.numel()
+    stage_ms = (ctypes.c_float * 5)()
+    stream = torch.cuda.current_stream(device).cuda_stream
+    elapsed = timed_region(
+        lambda: N.check(N.lib().mxa_attention_timed(ctypes.byref(p), stream, steps, stage_ms), "mxa_attention_timed"),
+        world, torch.cuda.synchronize, device)
+    stages = {"prep": float(stage_ms[0]), "dense": float(stage_ms[4])}
+    cb = dict(c, B=B)
+    tops = ops_gemm(cb) / (stages["dense"] * 1e-3) / 1e12
+    by = stage_bytes(cb, "rows_fused")["finish"]
+    extra = {"mfma": {"what": "SURVEY §8d Ops_gemm (QK^T + P.V int8 ops, every key) over the dense kernel's time",
+                      "ops": ops_gemm(cb), "achieved": tops, "peak": I8_PEAK_TOPS, "unit": "TOPS",
+                      "frac": tops / I8_PEAK_TOPS, "engine": fin_engines(p)},
+             "hbm": {"algorithmic_bytes_per_launch": by, "achieved": by / (stages["dense"] * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
+    if world == 1:  # one image against the oracle's dense branch (test infrastructure)
+        from oracle import mx_oracle as O
+        qh, kh, vh, bh = make_inputs(c, [images[0]])
+        r = O.attention(qh, kh, vh, c["scale"], top_k=False, pred_mode=c["mode"], bias=bh, flush=c["bias"])
+        extra["parity"] = {"out_normwise_rel_err": O.normwise_rel_err(out[:1].cpu().numpy(), r["out"]), "out_tol": 1e-3}
+    return elapsed, stages, extra
 
 
 def run_qkv(c, images, steps, warmup, device, world):
@@ -556,6 +613,15 @@ def run_secondary(args, c, rank, world, images, lines, run, device, res=None):
             {"config": args.config + "+qkv_linear+proj_linear", "workload": "x (B, N, C=%d) -> qkv mx.Linear -> MX "
              "top-k attention -> proj mx.Linear -> y (B, N, C), one call" % (c["H"] * c["D"]),
              "value": ptok / pel, "unit": "tokens/s", "ms_per_step": pel / psteps * 1e3, "stages_ms": pst, **pex})
+    if "dense" in lines and run is run_config:
+        # the dense branch (top_k=False) at the config's shape: QK^T and P.V over every key
+        nsteps = max(args.steps // 2, 1)
+        nel, nst, nex = run_dense(c, images, nsteps, 2, device, world)
+        ntok = (world * c["B"] if args.scaling == "weak" else c["B"]) * c["N"] * nsteps
+        res.setdefault("secondary", []).append(
+            {"config": args.config + "+dense", "workload": "the dense branch (top_k=False) of the %s shape: "
+             "softmax over every key's true score, MX(P) @ MX(V)" % args.config,
+             "value": ntok / nel, "unit": "tokens/s", "ms_per_step": nel / nsteps * 1e3, "stages_ms": nst, **nex})
     if args.config == "deit_base" and "dropin" in lines and run is run_config:
         # the drop-in modules the unchanged attention code imports (install_dropin)
         dsteps = max(args.steps // 4, 1)
@@ -617,10 +683,10 @@ def main(argv=None, run=run_config):
     ap.add_argument("--pmc-json", default=None,
                     help="PMC instruction counters per kernel (tools/pmc_summary.py --json; default: the "
                          "committed profiles/<PROFILE_TAG>_pmc_<config>.json)")
-    ap.add_argument("--lines", default="main,qkv,qkvproj,dropin,dit",
+    ap.add_argument("--lines", default="main,qkv,qkvproj,dense,dropin,dit",
                     help="which lines to run: main (the config), qkv (its fused qkv-Linear line), qkvproj (x -> "
-                         "qkv Linear -> attention -> proj Linear), dropin (the drop-in modules' path), dit "
-                         "(the DiT-XL/2 secondary of deit_base)")
+                         "qkv Linear -> attention -> proj Linear), dense (the top_k=False branch at the config's "
+                         "shape), dropin (the drop-in modules' path), dit (the DiT-XL/2 secondary of deit_base)")
     args = ap.parse_args(argv)
 
     env_world = os.environ.get("WORLD_SIZE")

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MXA_ABI_VERSION 4
+#define MXA_ABI_VERSION 5
 
 /* status codes */
 #define MXA_OK 0
@@ -211,6 +211,25 @@ int mxa_approx_scores(const mxa_attn_params* p, hipStream_t stream);
 #define MXA_PATH_ROWS_FUSED 2
 #define MXA_PATH_ROWS_SPLIT 3
 int mxa_attention_path(const mxa_attn_params* p);
+
+/*
+ * Which finishing kernel mxa_attention(p) runs, and so on which engines its two dense
+ * contractions (QK^T, P.V: microxscaling/mx/matmul.py:68-76, :85-88 as the callers use them,
+ * workloads/deit/scripts/main.py:124-152, workloads/DiT/models.py:194-225) run (no launch):
+ *   MXA_FIN_GATHER16    finish16_kernel: kept-key QK^T on v_dot4, P.V on v_mfma_i32_16x16x32_i8
+ *   MXA_FIN_GATHER32    finish_kernel: kept-key QK^T on v_dot4, P.V on v_mfma_i32_32x32x32_i8
+ *   MXA_FIN_MFMA        finish_qk_kernel: every key's QK^T and P.V on v_mfma_i32_16x16x32_i8
+ *                       (the prune mask applied in the softmax)
+ *   MXA_FIN_DENSE_MFMA  the dense branch (top_k == 0) on finish_qk_kernel, every key kept
+ *   MXA_FIN_DENSE_ROWS  the dense branch on dense_rows_kernel (T > 256): v_dot4 for both
+ * or a negative MXA_ERR_* for invalid parameters.
+ */
+#define MXA_FIN_GATHER16 1
+#define MXA_FIN_GATHER32 2
+#define MXA_FIN_MFMA 3
+#define MXA_FIN_DENSE_MFMA 4
+#define MXA_FIN_DENSE_ROWS 5
+int mxa_attention_finish_kernel(const mxa_attn_params* p);
 
 /*
  * Measurement entry point (bench.py): runs mxa_attention `iters` times on `stream`

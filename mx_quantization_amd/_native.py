@@ -21,10 +21,17 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
-ABI_VERSION = 4
+ABI_VERSION = 5
 DT_F32, DT_F16, DT_BF16 = 0, 1, 2
 DTYPES = {torch.float32: DT_F32, torch.float16: DT_F16, torch.bfloat16: DT_BF16}
 PATH_NAMES = {2: "rows_fused", 3: "rows_split"}  # mxa_attention_path
+# mxa_attention_finish_kernel: the finishing kernel and the engines of QK^T / P.V
+FIN_KERNELS = {1: ("finish16_kernel", "v_dot4 (kept keys)", "v_mfma_i32_16x16x32_i8"),
+               2: ("finish_kernel", "v_dot4 (kept keys)", "v_mfma_i32_32x32x32_i8"),
+               3: ("finish_qk_kernel", "v_mfma_i32_16x16x32_i8 (every key, prune mask in the softmax)",
+                   "v_mfma_i32_16x16x32_i8"),
+               4: ("finish_qk_kernel (dense: every key kept)", "v_mfma_i32_16x16x32_i8", "v_mfma_i32_16x16x32_i8"),
+               5: ("dense_rows_kernel", "v_dot4", "v_dot4")}
 PRED_MODES = {"ex_pred": 0, "partial_Q": 1, "partial_K": 2, "MXINT4": 3, "two_step_leading_ones": 4,
               "true_ex": 5, "ELSA": 6}
 ROUND_MODES = {"nearest": 0, "floor": 1, "even": 2}
@@ -75,6 +82,7 @@ _SIGS = {
     "mxa_attention": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_approx_scores": (c_i32, [ctypes.POINTER(AttnParams), c_vp]),
     "mxa_attention_path": (c_i32, [ctypes.POINTER(AttnParams)]),
+    "mxa_attention_finish_kernel": (c_i32, [ctypes.POINTER(AttnParams)]),
     "mxa_attention_timed": (c_i32, [ctypes.POINTER(AttnParams), c_vp, c_i32, ctypes.POINTER(c_f32)]),
     "mxa_linear_weight_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "mxa_linear_weight_prep": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),

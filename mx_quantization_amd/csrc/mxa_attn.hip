@@ -4,10 +4,13 @@
 //                               (mxa_quant.hip)
 //   cols_prep(V)                MXINT8 codes of V along tokens, stored [d][t]
 //   select_kernel               approximate scores + torch-CPU-order top-k, four query
-//                               rows per wave (mxa_select.hpp, mxa_topk_grp.hpp)
-//   finish_kernel               the kept keys' true scores, softmax, MX(P), P.V on int8
-//                               MFMA (mxa_finish.hpp)
-//   attn_rows2_kernel<..., 0>   the dense (top_k=False) branch (mxa_rows2.hpp)
+//                               rows per wave (mxa_select.hpp, mxa_topk_grp.hpp), the
+//                               one-lane tail (mxa_tail.hpp)
+//   finish16_kernel / finish_kernel / finish_qk_kernel
+//                               the kept keys' true scores, softmax, MX(P), P.V on int8
+//                               MFMA (mxa_finish16.hpp, mxa_finish.hpp, mxa_finish_qk.hpp)
+//   dense (top_k=False)         finish_qk_kernel with every key kept (T <= 256), else
+//                               dense_rows_kernel (mxa_rows2.hpp)
 //
 // This is the mx_quant branch of the patched attention forward:
 //   workloads/deit/scripts/main.py:100-152, workloads/DiT/models.py:168-225,
@@ -229,9 +232,10 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
 // scores_only: the approximate (or true) scores into p->pred_out / true_out, no top-k
 // xq: the fused qkv projection (q, k, v produced from x and the prepared weight)
 // pj: the proj Linear behind the attention (y = mx.Linear(out.transpose(1,2).reshape(B,N,C)))
+// fin (with plan): the finishing kernel (MXA_FIN_*, 0 for the scores alone)
 static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent_t* ev, int* plan = nullptr,
                           bool scores_only = false, const mxa_qkv_params* xq = nullptr,
-                          const mxa_proj_params* pj = nullptr) {
+                          const mxa_proj_params* pj = nullptr, int* fin = nullptr) {
   if (!p) return MXA_ERR_ARG;
   if (pj) {
     if (scores_only || !p->top_k || !pj->wq || !pj->y || pj->out_features <= 0 || pj->y_row_stride < pj->out_features)
@@ -303,6 +307,8 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
   if (rc) return rc;
   if (plan) {
     *plan = topk ? MXA_PATH_ROWS_SPLIT : MXA_PATH_ROWS_FUSED;
+    if (fin)
+      *fin = scores_only ? 0 : rows_kernel_kind(topk, r2.k_top, r2.T, r2.nbd, pj && proj_codes_direct(&pp));
     return MXA_OK;
   }
   if (!pp.workspace || pp.workspace_bytes < L.total) return MXA_ERR_WORKSPACE;
@@ -487,6 +493,12 @@ extern "C" int mxa_attention_path(const mxa_attn_params* p) {
   int plan = -1;
   const int rc = attention_impl(p, nullptr, nullptr, &plan);
   return rc ? rc : plan;
+}
+
+extern "C" int mxa_attention_finish_kernel(const mxa_attn_params* p) {
+  int plan = -1, fin = -1;
+  const int rc = attention_impl(p, nullptr, nullptr, &plan, false, nullptr, nullptr, &fin);
+  return rc ? rc : fin;
 }
 
 static int timed_impl(const mxa_attn_params* p, const mxa_qkv_params* xq, hipStream_t stream, int32_t iters,

@@ -1,6 +1,8 @@
 // Row-kernel launches: the finishing kernel of the top-k path (mxa_finish.hpp) and the
-// dense (top_k=False) row kernel (mxa_rows2.hpp).
+// dense (top_k=False) branch: the MFMA finishing kernel with every key kept
+// (mxa_finish_qk.hpp, T <= 256), else the row kernel (mxa_rows2.hpp).
 #include <algorithm>
+#include <atomic>
 
 #include "mxa_finish.hpp"
 #include "mxa_finish16.hpp"
@@ -146,12 +148,16 @@ template <int NB, int KS, int LPR, bool XDT>
 static int launch_finish16_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
   const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, LPR, XDT>);
-  static int regs_wps = 0;  // waves per SIMD the kernel's registers allow (per process: one device kind)
-  if (!regs_wps) {
+  // waves per SIMD the kernel's registers allow: a property of the code object (gfx950
+  // only), cached per instantiation; concurrent first launches compute the same value
+  static std::atomic<int> regs_wps{0};
+  int wps = regs_wps.load(std::memory_order_relaxed);
+  if (!wps) {
     hipFuncAttributes fa{};
-    regs_wps = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
+    wps = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
+    regs_wps.store(wps, std::memory_order_relaxed);
   }
-  int rc = finish16_plan(ra, BH, regs_wps, &ra.waves, &ra.rows_per_wg);
+  int rc = finish16_plan(ra, BH, wps, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
   const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -181,7 +187,8 @@ static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
 }
 
 static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (finish_qk_wanted(ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr)) {
+  const int kind = rows_kernel_kind(true, ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr);
+  if (kind == MXA_FIN_MFMA) {
     if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish_qk_x1(ra, BH, stream, plan);
     return launch_finish_qk_x0(ra, BH, stream, plan);
   }
@@ -191,7 +198,7 @@ static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool p
   // The proj's MX input codes (XO) stay on the 32-row kernel: its 32 x 32 output blocks are
   // whole MX blocks of the output rows (measured: 0.264 ms at DeiT-base against 0.308 ms
   // for 16-row tiles, whose 16 x 32 blocks take twice the transposes and syncs per row).
-  if (ra.k_top <= 64 && !ra.xo_codes) {
+  if (kind == MXA_FIN_GATHER16) {
     if (plan) {
       int w, r;
       return finish16_plan(ra, BH, 2, &w, &r);
@@ -222,6 +229,15 @@ int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, h
     Rows2Args rf = ra;
     if (true_mode) rf.true_out = nullptr;
     return launch_finish(rf, BH, stream, plan);
+  }
+  // the dense branch: the MFMA finishing kernel with every key kept (T <= 256: a row's scores
+  // in registers); longer rows: the v_dot4 row kernel
+  if (rows_kernel_kind(false, 0, ra.T, ra.nbd, false) == MXA_FIN_DENSE_MFMA) {
+    Rows2Args rd = ra;
+    rd.dense = 1;
+    rd.mask_out = nullptr;
+    if (rd.s_dt != kF32 || rd.in_dt != kF32) return launch_finish_qk_x1(rd, BH, stream, plan);
+    return launch_finish_qk_x0(rd, BH, stream, plan);
   }
   switch (S) {
     case 1: return launch_dense_s<1>(ra, BH, stream, plan);

@@ -3,6 +3,7 @@
 // (launch_finish_qk_x0), MXA_FQ_XDT=1 the float16 / bfloat16 ones (launch_finish_qk_x1),
 // so that the two build in parallel.
 #include <algorithm>
+#include <atomic>
 
 #include "mxa_finish_qk.hpp"
 #include "mxa_launch.hpp"
@@ -47,16 +48,20 @@ static int finish_qk_plan(const Rows2Args& ra, int nb, int BH, int regs_waves_pe
 template <int NB, int NTB, bool XDT>
 static int launch_finish_qk_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
-  if (!ra.mask_out || fq_ntb_max(ra.ntb) != NTB || ra.nbd != NB || ra.dpad != 32 * NB) return MXA_ERR_ARG;
+  if ((!ra.mask_out && !ra.dense) || fq_ntb_max(ra.ntb) != NTB || ra.nbd != NB || ra.dpad != 32 * NB) return MXA_ERR_ARG;
   const bool extra = ra.bias || ra.true_out || (ra.bfloat != 0 && ra.bfloat != 32);
   const void* fn = extra ? reinterpret_cast<const void*>(&finish_qk_kernel<NB, NTB, XDT, true>)
                          : reinterpret_cast<const void*>(&finish_qk_kernel<NB, NTB, XDT, false>);
-  static int regs_wps[2] = {0, 0};  // waves per SIMD the registers allow (per process: one device kind)
-  if (!regs_wps[extra]) {
+  // waves per SIMD the registers allow: a property of the code object (gfx950 only), cached
+  // per instantiation; concurrent first launches compute the same value
+  static std::atomic<int> regs_wps[2] = {0, 0};
+  int wps = regs_wps[extra].load(std::memory_order_relaxed);
+  if (!wps) {
     hipFuncAttributes fa{};
-    regs_wps[extra] = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
+    wps = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
+    regs_wps[extra].store(wps, std::memory_order_relaxed);
   }
-  int rc = finish_qk_plan(ra, NB, BH, regs_wps[extra], &ra.waves, &ra.rows_per_wg);
+  int rc = finish_qk_plan(ra, NB, BH, wps, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
   const size_t lds = fq_lds(ra.ntb, NB, NTB, ra.D).total;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

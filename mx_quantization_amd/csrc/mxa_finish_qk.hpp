@@ -21,6 +21,9 @@
 // maxima, an LDS P tile): no gather, no per-wave LDS, no kept-index read (the 8-word mask
 // per row instead of k indices), at the price of scoring the dropped keys too -- a win
 // once k is a large fraction of T.
+// The dense branch (top_k=False, Rows2Args::dense) is this kernel with every key < T kept:
+// attn = softmax(true scores) over the whole row, then MX(P) . MX(V) (deit main.py:149-152,
+// DiT models.py:218-225).
 // Reference: microxscaling/mx/matmul.py:68-76, :85-88 (the MX matmuls QK^T and P.V),
 // callers workloads/DiT/models.py:168-225 (gather :194-195), workloads/deit/scripts/main.py:
 // 124-152, workloads/PixArt/models/MX_transformer_block.py:679-717.
@@ -241,9 +244,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t kw[(NTB + 3) / 4];
 #pragma unroll
     for (int w = 0; w < (NTB + 3) / 4; ++w) kw[w] = 0u;
+    if (a.dense) {  // the dense branch: every key < T (wave-uniform)
 #pragma unroll
-    for (int blk = 0; blk < NTB; ++blk)
-      if (blk < ntb && valid) kw[blk >> 2] |= ((a.mask_out[grow * ntw + blk] >> (8 * g)) & 0xFFu) << (8 * (blk & 3));
+      for (int blk = 0; blk < NTB; ++blk) {
+        const int n = min(max(T - (32 * blk + 8 * g), 0), 8);
+        if (blk < ntb && valid) kw[blk >> 2] |= ((1u << n) - 1u) << (8 * (blk & 3));
+      }
+    } else {
+#pragma unroll
+      for (int blk = 0; blk < NTB; ++blk)
+        if (blk < ntb && valid) kw[blk >> 2] |= ((a.mask_out[grow * ntw + blk] >> (8 * g)) & 0xFFu) << (8 * (blk & 3));
+    }
     auto kept = [&](int blk, int j) { return (kw[blk >> 2] >> (8 * (blk & 3) + j)) & 1u; };
 
     // ---- 1. scores of every key; the kept ones enter the softmax ------------------------

@@ -50,7 +50,23 @@ inline int launch_select_mode(const Rows2Args& ra, int mode, int BH, hipStream_t
 // share of T (above the 16-row gather kernel's k <= 64), T <= 256 (the scores of a row in
 // registers); not with the proj Linear's MX input codes (xo).  It reads the selection's
 // prune-mask words (the caller's mask_out, else a workspace copy), not the kept indices.
-inline bool finish_qk_wanted(int k, int T, int nbd, bool xo) { return k >= 65 && T <= 256 && nbd <= 4 && !xo; }
+// (MXA_FQ_KMIN: a tools-only build of the threshold for same-box A/Bs, build_native defines)
+#ifndef MXA_FQ_KMIN
+#define MXA_FQ_KMIN 65
+#endif
+inline bool finish_qk_wanted(int k, int T, int nbd, bool xo) { return k >= MXA_FQ_KMIN && T <= 256 && nbd <= 4 && !xo; }
+// the dense branch (top_k=False) on the same kernel with every key kept (Rows2Args::dense)
+inline bool finish_qk_dense_ok(int T, int nbd) { return T <= 256 && nbd <= 4; }
+// the finishing kernel of a call (include/mxa.h MXA_FIN_*): the single decision launch_rows
+// (mxa_fin.hip) dispatches on and mxa_attention_finish_kernel reports
+inline int rows_kernel_kind(bool topk, int k, int T, int nbd, bool xo) {
+  if (!topk) return finish_qk_dense_ok(T, nbd) ? MXA_FIN_DENSE_MFMA : MXA_FIN_DENSE_ROWS;
+  if (finish_qk_wanted(k, T, nbd, xo)) return MXA_FIN_MFMA;
+  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k, and
+  // the proj's MX input codes (32 x 32 output tiles = whole MX blocks of the output rows):
+  // the 32-row kernel
+  return k <= 64 && !xo ? MXA_FIN_GATHER16 : MXA_FIN_GATHER32;
+}
 // its launches (mxa_fin_qk.hip): float32 inputs and scores (x0), float16 / bfloat16 (x1)
 int launch_finish_qk_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
 int launch_finish_qk_x1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);

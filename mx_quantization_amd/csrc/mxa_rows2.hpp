@@ -55,6 +55,9 @@ struct Rows2Args {
   // codes [B*N][H*D], code-unit exponents [B*N][H*D/32] -- instead of fp32 in `out`
   int8_t* xo_codes;
   int16_t* xo_exps;
+  // the dense branch (top_k=False) on the MFMA finishing kernel (mxa_finish_qk.hpp): every
+  // key < T kept, no prune-mask words read
+  int dense;
 };
 
 // words of a one-lane top-k tail staging record (mxa_tail.hpp): state, pad, TW elements

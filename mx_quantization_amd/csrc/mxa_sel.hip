@@ -54,10 +54,8 @@ template <int NP, int MODE, int W>
 static int launch_select_packed(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
   const int tw = sel_tail_width(MODE, ra.T, ra.k_top, ra.bias != nullptr);
   int rc;
-  if (tw == 32) {
-    rc = launch_select_w<NP, MODE, W, uint32_t, 1, 32>(ra, BH, stream, plan);
-    if (rc == MXA_OK) rc = launch_tail<32>(ra, BH, stream, plan);
-  } else if (tw == 64) {
+  static_assert(kTailPref == 64, "the one-lane tail is instantiated for a 64-position prefix");
+  if (tw == 64) {
     rc = launch_select_w<NP, MODE, W, uint32_t, 1, 64>(ra, BH, stream, plan);
     if (rc == MXA_OK) rc = launch_tail<64>(ra, BH, stream, plan);
   } else {
@@ -222,11 +220,9 @@ extern "C" int mxa_topk_ws(const void* vals, int64_t rows, int32_t n, int64_t ld
   const int tw = topk_ws_tw(n, k);
   if (n <= 128) {
     if (tw == 64) return launch_topk_packed<128, 64>(ga, w, grid, stream);
-    if (tw == 32) return launch_topk_packed<128, 32>(ga, w, grid, stream);
     return launch_topk_packed<128, 0>(ga, w, grid, stream);
   }
   if (tw == 64) return launch_topk_packed<256, 64>(ga, w, grid, stream);
-  if (tw == 32) return launch_topk_packed<256, 32>(ga, w, grid, stream);
   return launch_topk_packed<256, 0>(ga, w, grid, stream);
 }
 

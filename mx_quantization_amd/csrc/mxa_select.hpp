@@ -494,8 +494,9 @@ __device__ __forceinline__ void sel_mask_words(const Rows2Args& a, __attribute__
 // tail kernel (mxa_tail.hpp): their state and prefix are written to a.tail_rec (and the
 // first kept index set to 0, so the 64-bit pass leaves them alone); it writes their
 // indices and mask words.
+// Returns (per lane) whether this lane's row was left for the 64-bit pass.
 template <int NP, int MODE, typename El, int QM, int TW = 0>
-__device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, unsigned char* g0, int bh, int rq,
+__device__ __forceinline__ bool sel_rows4(const Rows2Args& a, const SelTabs& t, unsigned char* g0, int bh, int rq,
                                           int r_end, int lane) {
   constexpr bool kPacked = sizeof(El) == 4;
   const int gi = lane >> 4, gl = lane & 15;
@@ -531,12 +532,14 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
       else g.A[j] = pack_ki(key, (uint32_t)j);
     }
 #endif
-  if (k <= 0) return;  // scores only
+  if (k <= 0) return false;  // scores only
+  bool left = false;
   if constexpr (kPacked) {  // this row's 16 lanes: any score that does not pack
     const uint64_t bw = __builtin_amdgcn_ballot_w64(bad != 0u);
     if (valid && ((bw >> (16 * gi)) & 0xFFFFull) != 0) {
       if (gl == 0) kept_put(a, grow * k, -1);
       valid = false;
+      left = true;
     }
   }
   wave_lds_sync();
@@ -564,6 +567,7 @@ __device__ __forceinline__ void sel_rows4(const Rows2Args& a, const SelTabs& t, 
   }
   if (a.mask_out) sel_mask_words(a, g.stk, grow, valid, gl, 16, k, [&](int p) { return GEl<El>::idx(g.A[p]); });
   wave_lds_sync();
+  return left;
 }
 
 // One workgroup's work item: head bh, query-row chunk y (rows y * rows_per_wg ...).
@@ -575,19 +579,18 @@ __device__ __forceinline__ bool select_item(const Rows2Args& a, unsigned char* s
   const SelLds L = sel_lds(MODE, a.T, a.D, a.kst, a.nbd);
   const SelTabs t = sel_stage<MODE>(a, smem, L, bh);
   unsigned char* g0 = smem + L.rows + (size_t)4 * wave * grp_row_bytes(grp_alloc(a.T), NP, sizeof(El));
+  // (packed) whether a row this thread's wave handled was left for the 64-bit pass: tracked
+  // per thread, not read back from idx -- other waves' kept_put(-1) need not be visible yet
+  bool left = false;
   for (int rq = r0 + 4 * wave; rq < r_end; rq += 4 * kSelWaves) {
     if (sizeof(El) == 8 && a.fb_only) {  // the rows of this group that are left
       const int r = min(rq + (lane >> 4), r_end - 1);
       if (__builtin_amdgcn_ballot_w64(rq + (lane >> 4) < r_end && kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0) == 0)
         continue;
     }
-    sel_rows4<NP, MODE, El, QM, TW>(a, t, g0, bh, rq, r_end, lane);
+    left |= sel_rows4<NP, MODE, El, QM, TW>(a, t, g0, bh, rq, r_end, lane);
   }
-  // (packed: a row left for the 64-bit pass has kept_get(row * k) < 0)
-  int left = 0;
-  if (sizeof(El) == 4 && a.k_top > 0)
-    for (int r = r0 + (int)threadIdx.x; r < r_end; r += blockDim.x) left |= kept_get(a, ((int64_t)bh * a.N + r) * a.k_top) < 0;
-  return __syncthreads_or(left) != 0;
+  return __syncthreads_or(left ? 1 : 0) != 0;
 }
 
 // Selection kernel, four query rows per wave.  El = uint64_t: rows of up to 512 keys,

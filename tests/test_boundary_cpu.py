@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(N.EXPORTS), "ctypes signatures out of sync with include/mxa.h"
-    assert lib.mxa_abi_version() == N.ABI_VERSION == 4
+    assert lib.mxa_abi_version() == N.ABI_VERSION == 5
 
 
 def test_status_strings_and_arg_errors():
@@ -129,6 +129,24 @@ def test_attention_path_selection_is_host_logic():
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 3, 197, 197, 64, 20, top_k=0))) == fused
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 600, 64, 5))) == -2  # T > 512
     assert lib.mxa_attention_path(ctypes.byref(_params(1, 1, 10, 60, 160, 5))) == -2  # D > 128
+
+
+def test_finishing_kernel_selection_is_host_logic():
+    """mxa_attention_finish_kernel: which finishing kernel (and so which engines for QK^T /
+    P.V) each bench shape and the dense branch run -- the value bench.py's mfma.engine
+    reports (no launch, no GPU)."""
+    import ctypes
+    from mx_quantization_amd import _native as N
+    fk = lambda *a, **kw: N.lib().mxa_attention_finish_kernel(ctypes.byref(_params(*a, **kw)))
+    assert fk(256, 12, 197, 197, 64, 20) == 1            # DeiT-base k = 20: finish16_kernel
+    assert fk(64, 16, 256, 256, 72, 154) == 3            # DiT-XL/2 k = 154: finish_qk_kernel (MFMA QK^T)
+    assert fk(8, 16, 256, 120, 72, 20, "MXINT4") == 1    # PixArt cross
+    assert fk(1, 2, 100, 300, 64, 100) == 2              # T > 256, k > 64: the 32-row gather kernel
+    assert fk(256, 12, 197, 197, 64, 20, top_k=0) == 4   # dense DeiT-base: MFMA for both contractions
+    assert fk(64, 16, 256, 256, 72, 154, top_k=0) == 4   # dense DiT-XL/2
+    assert fk(1, 2, 100, 300, 64, 20, top_k=0) == 5      # dense, T > 256: the v_dot4 row kernel
+    assert fk(1, 1, 10, 600, 64, 5) == -2                # T > 512
+    assert set(N.FIN_KERNELS) == {1, 2, 3, 4, 5}
 
 
 def test_analysis_hooks_vs_reference():

@@ -465,6 +465,75 @@ def test_expred_special_rows(M, k):
         _check_vs_oracle(got, r, name)
 
 
+@pytest.mark.parametrize("D", [32, 64, 72, 128])
+@pytest.mark.parametrize("N,T", [(197, 197), (256, 256), (77, 120), (5, 20), (40, 300)])
+def test_dense_branch_vs_oracle(M, D, N, T):
+    """The dense branch (top_k=False, deit main.py:149-152, DiT models.py:218-225): true scores
+    bit-exact, the output within tolerance, on the MFMA finishing kernel with every key kept
+    (T <= 256) and on the v_dot4 row kernel (T = 300); special rows: NaN / Inf inputs, a row
+    whose bias masks every key (-inf: softmax NaN), zero rows, a wide exponent spread."""
+    rng = np.random.default_rng(D * 7 + T)
+    B, H = 2, 3
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, T, D), dtype=np.float32)
+    q[0, 0, min(3, N - 1), 1] = np.nan
+    q[0, 1, min(4, N - 1), 0] = np.inf
+    kk[1, 0, 2, :] = 0.0
+    q[1, 1, 0, :] = 0.0
+    kk[1, 2, 1, D // 2:] *= np.float32(2.0 ** 30)
+    bias = np.zeros((B, 1, N, T), np.float32)
+    bias[:, :, :, T // 2:] = -10000.0
+    bias[1, 0, min(2, N - 1), :] = -np.inf
+    fk = M._native.lib().mxa_attention_finish_kernel
+    for bb in (None, bias):
+        out, idx, true_s, _ = M.mx_topk_attention(dev(q), dev(kk), dev(v), D ** -0.5, top_k=False, return_scores=True,
+                                                  bias=None if bb is None else dev(bb))
+        assert idx is None
+        r = O.attention(q, kk, v, D ** -0.5, top_k=False, bias=bb)
+        same(host(true_s), r["true"], "true")
+        o, ro = host(out), r["out"]
+        same(np.isnan(o), np.isnan(ro), "NaN rows")
+        fin = ~np.isnan(ro).any(-1)
+        assert O.normwise_rel_err(o[fin], ro[fin]) <= OUT_TOL
+    if T <= 256:
+        import ctypes
+        p, _, _, _ = M.ops._attn_params(dev(q), dev(kk), dev(v), D ** -0.5, 0, "ex_pred", False, False, None, False, 0,
+                                        None)
+        p.out = 16  # the query launches nothing
+        assert fk(ctypes.byref(p)) == 4  # MXA_FIN_DENSE_MFMA
+
+
+@pytest.mark.parametrize("mode,k", [("ex_pred", 20), ("ex_pred", 100), ("MXINT4", 20)])
+def test_packed_pass_fallback_rows(M, mode, k):
+    """Scattered query rows whose approximate scores do not pack into 32-bit elements (the
+    query's second MX block scaled by 2^20: every score needs more than 16 significant bits)
+    go from the packed selection pass to the 64-bit pass, next to rows the packed pass and
+    the one-lane tail finish, in the same workgroups.  Every head's idx and prune mask
+    against the oracle's libstdc++ top-k of the oracle's scores (mxa_select.hpp select_item:
+    the per-workgroup fallback flag)."""
+    rng = np.random.default_rng(11)
+    B, H, N, D = 8, 12, 197, 64
+    q = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    kk = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    v = rng.standard_normal((B, H, N, D), dtype=np.float32)
+    r = np.arange(N)
+    for b in range(B):
+        for h in range(H):
+            rows = r[(r * 7 + 3 * h + b) % 13 == 0]
+            q[b, h, rows, 32:] *= np.float32(2.0 ** 20)
+    out, idx, _, pred_s, mask = M.mx_topk_attention(dev(q), dev(kk), dev(v), 0.125, k_top=k, pred_mode=mode,
+                                                    return_scores=True, return_mask=True)
+    aq, ak = O.approx_operands(q, kk, mode)
+    pred_o = O.exact_matmul_f32(aq, np.swapaxes(ak, -1, -2))
+    same(host(pred_s), pred_o, "pred")
+    _, want = O.topk(pred_o.reshape(-1, N), k)
+    same(host(idx).reshape(-1, k), want, "idx")
+    same(host(M.unpack_mask(mask, N)).reshape(-1, N), O.prune_mask(want, N), "mask")
+    ro = O.attention(q[:1], kk[:1], v[:1], 0.125, k_top=k, pred_mode=mode)
+    assert O.normwise_rel_err(host(out[:1]), ro["out"]) <= OUT_TOL
+
+
 @pytest.mark.parametrize("mode", ["MXINT4", "two_step_leading_ones", "partial_Q", "partial_K"])
 @pytest.mark.parametrize("N,T,k", [(197, 197, 20), (77, 120, 77), (33, 256, 154)])
 def test_approx_modes_all_paths_vs_oracle(M, mode, N, T, k):
