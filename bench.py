@@ -672,6 +672,7 @@ def main(argv=None, run=run_config):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="deit_base", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
+    ap.add_argument("--k", type=int, default=None, help="override the config's k (A/B runs only)")
     ap.add_argument("--cpu-images", type=int, default=-1, help="images for the CPU baseline (-1: the batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -697,7 +698,7 @@ def main(argv=None, run=run_config):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    c = CONFIGS[args.config]
+    c = CONFIGS[args.config] if args.k is None else dict(CONFIGS[args.config], k=args.k)
 
     cpu = None  # before any HIP call: the pool forks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
