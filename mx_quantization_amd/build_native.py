@@ -17,7 +17,11 @@ LIB = os.path.join(HERE, "libmxa.so")
 # one score mode's selection kernels each (MXA_SEL_PART), so that the parts build in parallel
 UNITS = [("mxa_quant.hip", "", ()), ("mxa_attn.hip", "", ()), ("mxa_sel.hip", "", ("MXA_SEL_PART=0",))]
 UNITS += [("mxa_sel.hip", f"_p{i}", (f"MXA_SEL_PART={i}",)) for i in range(1, 7)]
-UNITS += [("mxa_fin.hip", "", ()), ("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
+# mxa_fin.hip: the dispatch + dense kernel (part 0) and the 32-row finishing kernel per NB (1..4)
+UNITS += [("mxa_fin.hip", "", ("MXA_FIN_PART=0",))] + [("mxa_fin.hip", f"_p{i}", (f"MXA_FIN_PART={i}",)) for i in range(1, 5)]
+# the 16-row finishing kernel: float32 and float16 / bfloat16 instantiations (MXA_F16_XDT)
+UNITS += [("mxa_fin16.hip", f"_x{i}", (f"MXA_F16_XDT={i}",)) for i in range(2)]
+UNITS += [("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 # the MFMA finishing kernel's float32 and float16 / bfloat16 instantiations (MXA_FQ_XDT)
 UNITS += [("mxa_fin_qk.hip", f"_x{i}", (f"MXA_FQ_XDT={i}",)) for i in range(2)]
 SOURCES = sorted({u[0] for u in UNITS})

@@ -5,10 +5,18 @@
 #include <atomic>
 
 #include "mxa_finish.hpp"
-#include "mxa_finish16.hpp"
 #include "mxa_launch.hpp"
 
+// Compiled five times (build_native.py, MXA_FIN_PART): part 0 the dispatch (launch_rows) and
+// the dense row kernel, parts 1..4 the 32-row finishing kernel for NB = 1..4 blocks per head
+// dim (launch_finish32_p<NB>), so that the instantiations build in parallel.
+#ifndef MXA_FIN_PART
+#define MXA_FIN_PART 0
+#endif
+
 namespace mxa {
+
+#if MXA_FIN_PART == 0
 
 // ---- the dense row kernel (mxa_rows2.hpp) ------------------------------------------
 static size_t rows2_total(const Rows2Args& ra, int W) {
@@ -44,6 +52,8 @@ static int launch_dense_s(const Rows2Args& ra0, int BH, hipStream_t stream, bool
   hipLaunchKernelGGL(dense_rows_kernel<S>, dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
+
+#endif  // MXA_FIN_PART == 0
 
 // ---- finishing kernel (mxa_finish.hpp): 32-row MFMA tiles, one per wave ------------
 // two lanes per query row (one pass per tile) when every row's kept keys fit 2 x 16 slots
@@ -118,107 +128,32 @@ static int launch_finish_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
   if (ks <= 16) return launch_finish_ks<NB, 16, false>(ra, BH, stream);
   return launch_finish_ks<NB, 32, false>(ra, BH, stream);
 }
-// ---- finishing kernel, 16-row tiles (mxa_finish16.hpp) --------------------------------
-// waves per workgroup: the fewest sequential tile rounds per CU -- workgroups per CU over
-// the concurrency the LDS and the kernel's registers allow, times each workgroup's rounds
-// over its tiles (a head's tiles round-robin over the waves: the K table staged once)
-static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, int* waves, int* rows_per_wg) {
-  const int tiles = (ra.N + kFin16 - 1) / kFin16;
-  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w).total; };
-  if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
-  int chunks = 1;
-  while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
-  const int tpc = (tiles + chunks - 1) / chunks;
-  const int64_t wgs_per_cu = ((int64_t)BH * chunks + 255) / 256;
-  const int wave_cap = 4 * std::max(1, std::min(8, regs_waves_per_simd));
-  int w = 1;
-  int64_t best = -1;
-  for (int c = 1; c <= std::min(8, tpc); ++c) {
-    const size_t t = lds(c);
-    if (t > 160 * 1024) break;
-    const int64_t conc = std::max<int64_t>(1, std::min<int64_t>(160 * 1024 / t, wave_cap / c));
-    const int64_t score = (wgs_per_cu + conc - 1) / conc * ((tpc + c - 1) / c);
-    if (best < 0 || score < best) best = score, w = c;
-  }
-  *waves = w;
-  *rows_per_wg = kFin16 * ((tiles + chunks - 1) / chunks);
-  return MXA_OK;
-}
-template <int NB, int KS, int LPR, bool XDT>
-static int launch_finish16_xdt(const Rows2Args& ra0, int BH, hipStream_t stream) {
-  Rows2Args ra = ra0;
-  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, LPR, XDT>);
-  // waves per SIMD the kernel's registers allow: a property of the code object (gfx950
-  // only), cached per instantiation; concurrent first launches compute the same value
-  static std::atomic<int> regs_wps{0};
-  int wps = regs_wps.load(std::memory_order_relaxed);
-  if (!wps) {
-    hipFuncAttributes fa{};
-    wps = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.numRegs > 0 ? 512 / ((fa.numRegs + 7) / 8 * 8) : 2;
-    regs_wps.store(wps, std::memory_order_relaxed);
-  }
-  int rc = finish16_plan(ra, BH, wps, &ra.waves, &ra.rows_per_wg);
-  if (rc) return rc;
-  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish16_kernel<NB, KS, LPR, XDT>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream, ra);
-  return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
-}
-template <int NB, int KS, int LPR>
-static int launch_finish16_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
-  if (ra.xo_codes) return MXA_ERR_UNSUPPORTED;  // the proj's input codes: the 32-row kernel
-  if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish16_xdt<NB, KS, LPR, true>(ra, BH, stream);
-  return launch_finish16_xdt<NB, KS, LPR, false>(ra, BH, stream);
-}
-template <int NB>
-static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
-  const int k = ra.k_top;
-  if (k <= 64) {  // four lanes per row: slots ceil(k / 4)
-    const int ks = (k + 3) / 4;
-    if (ks <= 2) return launch_finish16_ks<NB, 2, 4>(ra, BH, stream);
-    if (ks <= 4) return launch_finish16_ks<NB, 4, 4>(ra, BH, stream);
-    if (ks <= 8) return launch_finish16_ks<NB, 8, 4>(ra, BH, stream);
-    if (ks <= 12) return launch_finish16_ks<NB, 12, 4>(ra, BH, stream);
-    return launch_finish16_ks<NB, 16, 4>(ra, BH, stream);
-  }
-  return MXA_ERR_UNSUPPORTED;  // k > 64: the 32-row kernel (launch_finish)
-}
-
-static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  const int kind = rows_kernel_kind(true, ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr);
-  if (kind == MXA_FIN_MFMA) {
-    if (ra.s_dt != kF32 || ra.in_dt != kF32) return launch_finish_qk_x1(ra, BH, stream, plan);
-    return launch_finish_qk_x0(ra, BH, stream, plan);
-  }
-  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k
-  // (DiT's 154): the 32-row kernel (measured: DiT-XL/2 0.35 ms there vs 0.39 with
-  // 16-row tiles of sixteen lanes per row)
-  // The proj's MX input codes (XO) stay on the 32-row kernel: its 32 x 32 output blocks are
-  // whole MX blocks of the output rows (measured: 0.264 ms at DeiT-base against 0.308 ms
-  // for 16-row tiles, whose 16 x 32 blocks take twice the transposes and syncs per row).
-  if (kind == MXA_FIN_GATHER16) {
-    if (plan) {
-      int w, r;
-      return finish16_plan(ra, BH, 2, &w, &r);
-    }
-    switch (ra.nbd) {
-      case 1: return launch_finish16_nb<1>(ra, BH, stream);
-      case 2: return launch_finish16_nb<2>(ra, BH, stream);
-      case 3: return launch_finish16_nb<3>(ra, BH, stream);
-      default: return launch_finish16_nb<4>(ra, BH, stream);
-    }
-  }
+#if MXA_FIN_PART > 0
+#define MXA_FIN_FN2(i) launch_finish32_p##i
+#define MXA_FIN_FN(i) MXA_FIN_FN2(i)
+int MXA_FIN_FN(MXA_FIN_PART)(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
   if (plan) {
     int w, r;
     return finish_plan(ra, BH, &w, &r);
   }
+  return launch_finish_nb<MXA_FIN_PART>(ra, BH, stream);
+}
+#else
+static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
+  const int kind = rows_kernel_kind(true, ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr);
+  const bool xdt = ra.s_dt != kF32 || ra.in_dt != kF32;
+  if (kind == MXA_FIN_MFMA) return xdt ? launch_finish_qk_x1(ra, BH, stream, plan) : launch_finish_qk_x0(ra, BH, stream, plan);
+  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k with
+  // T > 256: the 32-row kernel.  The proj's MX input codes (XO) stay on the 32-row kernel:
+  // its 32 x 32 output blocks are whole MX blocks of the output rows (measured: 0.264 ms at
+  // DeiT-base against 0.308 ms for 16-row tiles, whose 16 x 32 blocks take twice the
+  // transposes and syncs per row).
+  if (kind == MXA_FIN_GATHER16) return xdt ? launch_finish16_x1(ra, BH, stream, plan) : launch_finish16_x0(ra, BH, stream, plan);
   switch (ra.nbd) {
-    case 1: return launch_finish_nb<1>(ra, BH, stream);
-    case 2: return launch_finish_nb<2>(ra, BH, stream);
-    case 3: return launch_finish_nb<3>(ra, BH, stream);
-    default: return launch_finish_nb<4>(ra, BH, stream);
+    case 1: return launch_finish32_p1(ra, BH, stream, plan);
+    case 2: return launch_finish32_p2(ra, BH, stream, plan);
+    case 3: return launch_finish32_p3(ra, BH, stream, plan);
+    default: return launch_finish32_p4(ra, BH, stream, plan);
   }
 }
 
@@ -246,6 +181,7 @@ int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, h
     default: return launch_dense_s<8>(ra, BH, stream, plan);
   }
 }
+#endif  // MXA_FIN_PART
 
 
 }  // namespace mxa

@@ -1,29 +1,27 @@
-// Finishing kernel of the top-k path, 16-ROW TILES: for every query row and its k
-// kept keys (the selection kernel's indices) the true scores, softmax, MX(P) along
-// keys and P.V, with P.V on v_mfma_i32_16x16x32_i8.
+// Finishing kernel of the top-k path for small k (k <= 64: DeiT's 20 / 30, PixArt's 20),
+// 16-ROW TILES: for every query row and its k kept keys (the selection kernel's indices) the
+// true scores, softmax, MX(P) along keys and P.V, with P.V on v_mfma_i32_16x16x32_i8.
 //
-// Why 16-row tiles (against the 32-row tiles of mxa_finish.hpp): the per-wave LDS is the
-// P code tile of the wave's rows, so halving the tile halves it, and the V^T operand is
-// read straight from HBM / L2 -- token-block-major V^T codes give each 16 x 32 MFMA B
-// operand as one contiguous 512-B run, so the loads coalesce -- instead of being staged
-// in LDS; only the head's K table (the gathered keys of the true scores) stays in LDS.
-// That lets twice the waves stay resident to hide the gather / softmax latency, which is
-// what bounds this kernel (SQ_WAIT_ANY, not the VALU or the MFMA, in the PMC passes).
-//
-// Per workgroup (one head, or a chunk of its query rows): the head's K codes + exponents
-// and the V block exponents staged in LDS once.  Per wave, tiles of 16 query rows:
-//   1. LPR = 4: the 16 rows in one pass, four lanes per row (k <= 4 KS; DeiT's k = 20);
-//      LPR = 16: four passes of four rows, one 16-lane DPP row per query row (DiT's
-//      k = 154).  Lane slots s, s + LPR, ...: the kept key's true score fl32(exact sum)
-//      * scale (+ bias) by v_dot4 over the LDS codes (exact block epilogue);
-//      softmax over the kept scores (DPP reductions); P MX-quantized along keys (block
-//      maxima by LDS atomic max) into the tile's dense code rows (zero elsewhere).
-//   2. P.V for the tile: per 16 output columns and per 32-key MX block ONE
-//      v_mfma_i32_16x16x32_i8 (K = 32 = one block: each block keeps its exact int32 sum),
-//      epilogue acc += C * (sP[row][b] * sV[b][d]) in fp32 (P.V is a tolerance-only
-//      product).
-//   3. the tile's output rows go out.  (The proj Linear's MX input codes stay on the
-//      32-row kernel, whose 32 x 32 output blocks are whole MX blocks of the rows.)
+// Per workgroup (one head, or a chunk of its query rows): the head's K codes + exponents and
+// the V block scales (as floats) staged in LDS once.  Per wave, tiles of 16 query rows, four
+// lanes per row, lane slots ph, ph + 4, ... (KS of them: k <= 4 KS):
+//   1. the kept key's true score fl32(exact sum) * scale (+ bias) by v_dot4 over the LDS codes
+//      (exact block epilogue); softmax over the kept scores (quad DPP); P
+//      MX-quantized along keys: block maxima by LDS atomic max, the block's code multiplier
+//      2^-es, the codes into the tile's dense code rows (zero elsewhere);
+//   2. P.V for the tile, key block outer: per 32-key MX block the P operand and row scales
+//      once, then per 16 output columns ONE v_mfma_i32_16x16x32_i8 (K = 32 = one block: each
+//      block keeps its exact int32 sum), epilogue acc += C * (sP[row][b] * sV[b][d]) in fp32
+//      (P.V is a tolerance-only product); the V^T operands (token-block-major
+//      codes: one contiguous 512-B run per MFMA) straight from HBM / L2, the next block's in
+//      flight while this block's MFMAs run;
+//   3. the tile's output rows go out; the written code positions are cleared.
+// Every slot runs the same instructions (an unused slot -- k < 4 KS, or a row past the end --
+// scores key 0 and writes its code to a pad column), so the per-slot work has no branches.
+// exp / divide: the softmax on v_exp_f32 (2^((v - mx) log2 e)) and a corrected reciprocal
+// (P is a tolerance-only operand, as in mxa_finish_qk.hpp).
+// (The proj Linear's MX input codes stay on the 32-row kernel, whose 32 x 32 output blocks
+// are whole MX blocks of the rows.)
 // Reference: microxscaling/mx/matmul.py:68-76 (MX P.V), callers
 // workloads/deit/scripts/main.py:124-152, workloads/DiT/models.py:195-225,
 // workloads/PixArt/models/MX_transformer_block.py:679-717, :826-859.
@@ -39,8 +37,9 @@ constexpr int kFin16Occ = 4;  // waves per SIMD the register allocation aims at
 
 typedef int v4i16_ __attribute__((ext_vector_type(4)));
 
-// LDS: tables (K codes, K exponents, V block exponents), then per wave the P code tile
-// [16][vst], the P block scales sP [ntb][16] (float), the block maxima bm [16][ntb] (u32)
+// LDS: tables (K codes, K exponents, V block scales as floats [ntb][D]), then per wave the P
+// code tile [16][vst] (columns >= tpad: the unused slots' pad), the P block scales sP
+// [ntb][16] (float), the block maxima / code multipliers bm [16][ntb] (u32)
 struct Fin16Lds {
   size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
 };
@@ -54,7 +53,7 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   o += al((size_t)T * nbd * 2);
   L.vt = o;
   L.ve = o;
-  o += al((size_t)ntb * D * 2);
+  o += al((size_t)ntb * D * 4);
   L.waves = o;
   L.sp = al((size_t)kFin16 * vst);
   L.bm = L.sp + al((size_t)ntb * kFin16 * 4);
@@ -63,9 +62,12 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   return L;
 }
 
-template <int NB, int KS, int LPR, bool XDT>
+// NB: 32-blocks per head dim; KS: kept slots per lane (k <= 4 KS); XDT: float16 / bfloat16
+// inputs or scores (the dtype roundings at run time); EXTRA: a bias, the debug true-score
+// output or bfloatX rounding (else the scores and P are plain float32)
+template <int NB, int KS, bool XDT, bool EXTRA>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && KS <= 12 ? kFin16Occ : (NB * KS <= 64 ? 3 : 2), 8))) void finish16_kernel(Rows2Args a) {
-  static_assert(LPR == 4 || LPR == 16, "four or sixteen lanes per query row");
+  constexpr bool kRound = XDT || EXTRA;
   const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -76,16 +78,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   const Fin16Lds L = fin16_lds(T, D, kst, nbd, vst, ntb, a.waves);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
-  int16_t* tve = reinterpret_cast<int16_t*>(smem + L.ve);
+  float* tvs = reinterpret_cast<float*>(smem + L.ve);
   unsigned char* wb = smem + L.waves + (size_t)wave * L.per_wave;
   int8_t* ptile = reinterpret_cast<int8_t*>(wb);
   float* sP = reinterpret_cast<float*>(wb + L.sp);
-  // the lane's query row within its pass (LPR 4: the tile row; LPR 16: the pass row)
-  // and its slot phase
-  const int pr = LPR == 4 ? lane >> 2 : lane >> 4, ph = LPR == 4 ? lane & 3 : lane & 15;
   uint32_t* bmw = reinterpret_cast<uint32_t*>(wb + L.bm);  // [16][ntb]
+  const int pr = lane >> 2, ph = lane & 3;  // the lane's tile row and slot phase
 
-  // ---- stage the head's K table and V block exponents; clear the code tile ---------
+  // ---- stage the head's K table and V block scales; clear the code tile ---------------
   const int64_t kb = (int64_t)bh * T;
   {
     const int cpr = a.dpad / 16;
@@ -96,177 +96,180 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     }
     for (int i = threadIdx.x; i < T * nbd; i += blockDim.x) tke[i] = a.ksT[kb * nbd + i];
     const int16_t* vssrc = a.vs + (int64_t)bh * ntb * D;
-    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tve[i] = vssrc[i];
+    for (int i = threadIdx.x; i < ntb * D; i += blockDim.x) tvs[i] = scale_f(exp_from16(vssrc[i]));
     for (int i = lane; i < kFin16 * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
     for (int i = lane; i < kFin16 * ntb; i += 64) bmw[i] = 0u;
   }
   __syncthreads();
 
   const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
-  constexpr int kPasses = LPR == 4 ? 1 : kFin16 / 4;
-  // a pass's global inputs (the row's query codes / exponents and kept indices); loaded
-  // at the start of the pass -- the resident waves hide their latency (a copy loaded one
-  // pass ahead costs the registers of a resident wave)
-  struct PassIn {
+  uint32_t* bm = bmw + pr * ntb;
+  const int pad = a.tpad + ph;  // an unused slot's code column (never read by the MFMA)
+  const int ln = lane & 15, kg = lane >> 4;
+  const int8_t* vbase = a.vt + (int64_t)bh * D * a.tpad + 8 * kg;
+  constexpr int NDT = 2 * NB;  // 16-column tiles of D <= 32 NB
+  for (int r0 = r_beg + kFin16 * wave; r0 < r_end; r0 += kFin16 * a.waves) {
+    const int r = r0 + pr;
+    const bool valid = r < r_end;
+    const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
+    const int64_t brow = EXTRA && a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
+    // the row's query codes / exponents and its kept indices
     uint4 qv[2 * NB];
     int qe[NB];
-    int ix[KS];
-  };
-  auto load_pass = [&](int r0, int pass, PassIn& in) {
-    const int r = r0 + (LPR == 4 ? pr : 4 * pass + pr);
-    const bool valid = r < r_end;
-    const int64_t grow = (int64_t)bh * a.N + (valid ? r : r_beg);
-    const int8_t* qsrc = a.qc + grow * a.dpad;
+    {
+      const int8_t* qsrc = a.qc + grow * a.dpad;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      in.qv[2 * b] = *reinterpret_cast<const uint4*>(qsrc + 32 * b);
-      in.qv[2 * b + 1] = *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16);
-      in.qe[b] = exp_from16(a.qsT[grow * nbd + b]);
+      for (int b = 0; b < NB; ++b) {
+        qv[2 * b] = *reinterpret_cast<const uint4*>(qsrc + 32 * b);
+        qv[2 * b + 1] = *reinterpret_cast<const uint4*>(qsrc + 32 * b + 16);
+        qe[b] = exp_from16(a.qsT[grow * nbd + b]);
+      }
     }
+    int ix[KS];
+    bool on[KS];
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
-      const int s = ph + LPR * t;
-      in.ix[t] = valid && s < k ? kept_get(a, grow * k + s) : -1;
+      const int s = ph + 4 * t;
+      on[t] = valid && s < k;
+      ix[t] = on[t] ? kept_get(a, grow * k + s) : 0;
     }
-  };
+    auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
+      const float acc = true_dot<NB>(qv, qe, tkc + (size_t)j * kst, tke + j * nbd);
+      if (!kRound) return acc * a.scale;
+      float t = round_bfloat(round_dt(acc, sdt), a.bfloat, kRoundNearest, 1, sdt);
+      t = round_dt(t * a.scale, sdt);
+      if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);
+      return t;
+    };
+    if (EXTRA && a.true_out && valid)  // debug output: every key's true score
+      for (int j = ph; j < T; j += 4) a.true_out[grow * T + j] = true_of(j);
 
-  for (int r0 = r_beg + kFin16 * wave; r0 < r_end; r0 += kFin16 * a.waves) {
     // ---- 1. kept scores, softmax, MX(P) into the code tile ------------------------------
-    for (int pass = 0; pass < kPasses; ++pass) {
-      PassIn cur;
-      load_pass(r0, pass, cur);
-      const int tr = LPR == 4 ? pr : 4 * pass + pr;  // row within the tile
-      const int r = r0 + tr;
-      const bool valid = r < r_end;
-      const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
-      const int64_t brow = a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
-      auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
-        const float acc = true_dot<NB>(cur.qv, cur.qe, tkc + (size_t)j * kst, tke + j * nbd);
-        float t = round_bfloat(round_dt(acc, sdt), a.bfloat, kRoundNearest, 1, sdt);
-        t = round_dt(t * a.scale, sdt);
-        if (brow >= 0) t = round_dt(t + load_dt(a.bias, brow + (int64_t)j * a.bs3, idt), sdt);
-        return t;
-      };
-      if (a.true_out && valid)  // debug output: every key's true score
-        for (int j = ph; j < T; j += LPR) a.true_out[grow * T + j] = true_of(j);
-      auto rmax = [](float x) {
-        uint32_t u = __float_as_uint(x);
-        auto op = [](uint32_t p, uint32_t q) { return __float_as_uint(fmaxf(__uint_as_float(p), __uint_as_float(q))); };
-        u = op(u, dpp_u32<0xB1>(u));
-        u = op(u, dpp_u32<0x4E>(u));
-        if (LPR == 16) {
-          u = op(u, dpp_u32<0x141>(u));
-          u = op(u, dpp_u32<0x140>(u));
-        }
-        return __uint_as_float(u);
-      };
-      auto rsum = [](float x) {
-        uint32_t u = __float_as_uint(x);
-        auto op = [](uint32_t p, uint32_t q) { return __float_as_uint(__uint_as_float(p) + __uint_as_float(q)); };
-        u = op(u, dpp_u32<0xB1>(u));
-        u = op(u, dpp_u32<0x4E>(u));
-        if (LPR == 16) {
-          u = op(u, dpp_u32<0x141>(u));
-          u = op(u, dpp_u32<0x140>(u));
-        }
-        return __uint_as_float(u);
-      };
-      float v[KS];
-      float mx = -INFINITY;
+    float v[KS];
+    float mx = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < KS; ++t) {
-        v[t] = cur.ix[t] >= 0 ? true_of(cur.ix[t]) : -INFINITY;
-        mx = fmaxf(mx, v[t]);
-      }
-      mx = rmax(mx);
-      float sum = 0.0f;
+    for (int t = 0; t < KS; ++t) {
+      const float s = true_of(ix[t]);
+      v[t] = on[t] ? s : -INFINITY;
+      mx = fmaxf(mx, v[t]);
+    }
+    auto qmax = [](float x) {
+      uint32_t u = __float_as_uint(x);
+      auto op = [](uint32_t p, uint32_t q) { return __float_as_uint(fmaxf(__uint_as_float(p), __uint_as_float(q))); };
+      u = op(u, dpp_u32<0xB1>(u));
+      return __uint_as_float(op(u, dpp_u32<0x4E>(u)));
+    };
+    auto qsum = [](float x) {
+      uint32_t u = __float_as_uint(x);
+      auto op = [](uint32_t p, uint32_t q) { return __float_as_uint(__uint_as_float(p) + __uint_as_float(q)); };
+      u = op(u, dpp_u32<0xB1>(u));
+      return __uint_as_float(op(u, dpp_u32<0x4E>(u)));
+    };
+    mx = qmax(mx);
+    // exp(v - mx) as 2^((v - mx) log2 e) (the difference first: folding mx log2 e into an
+    // fma loses the argument for large scores); an unused slot adds 0 (also where mx = -inf)
+    float sum = 0.0f;
 #pragma unroll
-      for (int t = 0; t < KS; ++t) {
-        v[t] = cur.ix[t] >= 0 ? expf(v[t] - mx) : 0.0f;
-        sum += v[t];
-      }
-      sum = rsum(sum);
-      // zeros.scatter_(idx, softmax) -> MXINT8 along keys (block maxima by atomic max)
-      uint32_t* bm = bmw + tr * ntb;
+    for (int t = 0; t < KS; ++t) {
+      v[t] = on[t] ? __builtin_amdgcn_exp2f((v[t] - mx) * 1.4426950408889634f) : 0.0f;
+      sum += v[t];
+    }
+    sum = qsum(sum);
+    // p = v / sum from y = RN(1 / sum): q = RN(v y), r = v - q sum exact by fma, RN(q + r y)
+    const float rs = 1.0f / sum;
 #pragma unroll
-      for (int t = 0; t < KS; ++t) {
-        if (cur.ix[t] >= 0) {
-          v[t] = round_dt(round_bfloat(v[t] / sum, a.bfloat, kRoundNearest, 1, sdt), sdt);
-          atomicMax(&bm[cur.ix[t] >> 5], __float_as_uint(v[t]) & 0x7FFFFFFFu);
+    for (int t = 0; t < KS; ++t) {
+      const float q0 = v[t] * rs;
+      float p = __builtin_fmaf(__builtin_fmaf(-q0, sum, v[t]), rs, q0);
+      if (kRound) p = round_dt(round_bfloat(p, a.bfloat, kRoundNearest, 1, sdt), sdt);
+      v[t] = p;
+      // zeros.scatter_(idx, softmax) -> MXINT8 along keys: the block maxima (an unused slot
+      // adds max(., 0) to block 0: no change)
+      atomicMax(&bm[ix[t] >> 5], __float_as_uint(p) & 0x7FFFFFFFu);
+    }
+    wave_lds_sync();
+    // per block: the scale sP (NaN for a NaN block) and the code multiplier 2^-es (0 for a NaN
+    // or flushed block: its codes 0; XDT: es + 1024 and the flush flag, round_code at run time)
+    for (int bk = ph; bk < ntb; bk += 4) {
+      int e_raw;
+      const int es = scale_exponent_dt(bm[bk], 127, sdt, &e_raw);
+      const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
+      sP[bk * kFin16 + pr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
+      if (XDT) bm[bk] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
+      else bm[bk] = __float_as_uint(es == kExpNaN || fl ? 0.0f : pow2f(-es));
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const uint32_t e = bm[ix[t] >> 5];
+      int code;
+      if (XDT) {
+        code = 0;
+        if (e & 0xFFFFu) {
+          const int es = (int)(e & 0xFFFFu) - 1024;
+          const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
+          code = (int)round_code(x, es, 8, kRoundNearest, sdt);
         }
+      } else {  // round_code for p >= 0: floor(p 2^-es 64 + 0.5), <= 127 (a NaN block: sP is NaN)
+        const float y = (v[t] * __uint_as_float(e)) * 64.0f;
+        code = (int)fminf(floorf(y + 0.5f), 127.0f);
       }
-      wave_lds_sync();
-      for (int bk = ph; bk < ntb; bk += LPR) {  // block bk: scale exponent (+1024; 0 = NaN block), flush flag
-        int e_raw;
-        const int es = scale_exponent_dt(bm[bk], 127, sdt, &e_raw);
-        const bool fl = a.flush_p && !(e_raw != kExpNaN && e_raw > -127);
-        sP[bk * kFin16 + tr] = scale_f(es == kExpNaN ? kExpNaN : es - 6);
-        bm[bk] = (es == kExpNaN ? 0u : (uint32_t)(es + 1024)) | (fl ? 0x10000u : 0u);
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int t = 0; t < KS; ++t) {
-        if (cur.ix[t] >= 0) {
-          const uint32_t e = bm[cur.ix[t] >> 5];
-          int code = 0;
-          if (e & 0xFFFFu) {
-            const int es = (int)(e & 0xFFFFu) - 1024;
-            const float x = (e & 0x10000u) ? v[t] * 0.0f : v[t];
-            code = (int)round_code(x, es, 8, kRoundNearest, sdt);
-          }
-          ptile[tr * vst + cur.ix[t]] = (int8_t)code;
-        }
-      }
-      wave_lds_sync();
-      for (int bk = ph; bk < ntb; bk += LPR) bm[bk] = 0u;
+      ptile[pr * vst + (on[t] ? ix[t] : pad)] = (int8_t)code;
     }
     wave_lds_sync();
 
-    // ---- 2. P.V on int8 MFMA: one v_mfma_i32_16x16x32_i8 per (16 columns, key block) ----
+    // ---- 2. P.V on int8 MFMA, key block outer -----------------------------------------------
     // lane maps (checked on hardware by mxa_selftest_mfma): A[m][k], m = lane % 16,
     // k = 8 (lane / 16) + 0..7; B[k][n], n = lane % 16, the same k; C[m][n] in c[i],
-    // m = 4 (lane / 16) + i, n = lane % 16.  B (V^T) straight from memory: the head's
-    // codes are [ntb][D][32], so the operand of (block b, columns dt..dt+15) is one
-    // contiguous 512-B run.
-    const int ln = lane & 15, kg = lane >> 4;
-    const int8_t* vbase = a.vt + (int64_t)bh * D * a.tpad + 8 * kg;
-    for (int dt = 0; dt < D; dt += 16) {
-      const int d = min(dt + ln, D - 1);
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int b0 = 0; b0 < ntb; b0 += 4) {  // the B operands of up to 4 blocks in flight
-        int64_t bv[4];
+    // m = 4 (lane / 16) + i, n = lane % 16.  A = the P code rows, B = V^T: the head's codes
+    // are [ntb][D][32], so the operand of (block b, columns 16 u ..) is one contiguous 512-B run
+    float acc[NDT][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (b0 + u < ntb) bv[u] = *reinterpret_cast<const int64_t*>(vbase + ((int64_t)(b0 + u) * D + d) * 32);
+    for (int u = 0; u < NDT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = acc[u][3] = 0.0f;
+    int64_t bv[NDT];
+    auto load_v = [&](int b, int64_t* dst) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int b = b0 + u;
-          if (b < ntb) {
-            const int64_t av = *reinterpret_cast<const int64_t*>(ptile + ln * vst + 32 * b + 8 * kg);
-            const v4i16_ zero = {0, 0, 0, 0};
-            const v4i16_ c = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv[u], zero, 0, 0, 0);
-            const float sv = scale_f(exp_from16(tve[b * D + d]));
-            const float4 s4 = *reinterpret_cast<const float4*>(sP + b * kFin16 + 4 * kg);
-            acc[0] = fmaf((float)c[0], s4.x * sv, acc[0]);
-            acc[1] = fmaf((float)c[1], s4.y * sv, acc[1]);
-            acc[2] = fmaf((float)c[2], s4.z * sv, acc[2]);
-            acc[3] = fmaf((float)c[3], s4.w * sv, acc[3]);
-          }
+      for (int u = 0; u < NDT; ++u)
+        if (16 * u < D) dst[u] = *reinterpret_cast<const int64_t*>(vbase + ((int64_t)b * D + min(16 * u + ln, D - 1)) * 32);
+    };
+    load_v(0, bv);
+    for (int b = 0; b < ntb; ++b) {
+      int64_t bn[NDT];
+      if (b + 1 < ntb) load_v(b + 1, bn);  // the next block's operands in flight
+      const int64_t av = *reinterpret_cast<const int64_t*>(ptile + ln * vst + 32 * b + 8 * kg);
+      const float4 s4 = *reinterpret_cast<const float4*>(sP + b * kFin16 + 4 * kg);
+#pragma unroll
+      for (int u = 0; u < NDT; ++u) {
+        if (16 * u < D) {
+          const v4i16_ zero = {0, 0, 0, 0};
+          const v4i16_ c = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv[u], zero, 0, 0, 0);
+          const float sv = tvs[b * D + min(16 * u + ln, D - 1)];
+          acc[u][0] = fmaf((float)c[0], s4.x * sv, acc[u][0]);
+          acc[u][1] = fmaf((float)c[1], s4.y * sv, acc[u][1]);
+          acc[u][2] = fmaf((float)c[2], s4.z * sv, acc[u][2]);
+          acc[u][3] = fmaf((float)c[3], s4.w * sv, acc[u][3]);
         }
       }
-      // ---- 3. output rows (64-B segments per row) ------------------------------------
-      if (dt + ln < D) {
+#pragma unroll
+      for (int u = 0; u < NDT; ++u) bv[u] = bn[u];
+    }
+    // ---- 3. output rows (64-B segments per row); clear the written code positions ---------
+#pragma unroll
+    for (int u = 0; u < NDT; ++u) {
+      if (16 * u + ln < D) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = r0 + 4 * kg + i;
-          if (r < r_end)
-            store_dt(a.out, b_ * a.os0 + h_ * a.os1 + (int64_t)r * a.os2 + dt + ln,
-                     round_bfloat(round_dt(acc[i], sdt), a.bfloat, kRoundNearest, 1, sdt), sdt);
+          const int rr = r0 + 4 * kg + i;
+          if (rr < r_end)
+            store_dt(a.out, b_ * a.os0 + h_ * a.os1 + (int64_t)rr * a.os2 + 16 * u + ln,
+                     kRound ? round_bfloat(round_dt(acc[u][i], sdt), a.bfloat, kRoundNearest, 1, sdt) : acc[u][i], sdt);
         }
       }
     }
-    wave_lds_sync();
-    for (int i = lane; i < kFin16 * vst / 16; i += 64) reinterpret_cast<uint4*>(ptile)[i] = make_uint4(0, 0, 0, 0);
+    wave_lds_sync();  // every lane's MFMA reads of the tile are done
+#pragma unroll
+    for (int t = 0; t < KS; ++t) ptile[pr * vst + (on[t] ? ix[t] : pad)] = 0;
+    for (int bk = ph; bk < ntb; bk += 4) bm[bk] = 0u;
     wave_lds_sync();
   }
 }

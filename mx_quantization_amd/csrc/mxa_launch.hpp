@@ -70,6 +70,14 @@ inline int rows_kernel_kind(bool topk, int k, int T, int nbd, bool xo) {
 // its launches (mxa_fin_qk.hip): float32 inputs and scores (x0), float16 / bfloat16 (x1)
 int launch_finish_qk_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
 int launch_finish_qk_x1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+// the 16-row finishing kernel (mxa_fin16.hip): float32 (x0), float16 / bfloat16 (x1)
+int launch_finish16_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+int launch_finish16_x1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+// the 32-row finishing kernel for NB blocks per head dim (mxa_fin.hip parts 1..4)
+int launch_finish32_p1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+int launch_finish32_p2(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+int launch_finish32_p3(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
+int launch_finish32_p4(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
 // the row kernel of the path: finishing kernel (top-k) or dense row kernel (mxa_fin.hip)
 int launch_rows(const Rows2Args& ra, bool topk, bool true_mode, int S, int BH, hipStream_t stream, bool plan);
 // fused qkv projection kernel (mxa_proj.hip)
