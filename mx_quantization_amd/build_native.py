@@ -62,16 +62,21 @@ def _obj_stale(obj, dep, cmd_file, cmd):
     return any(not os.path.exists(x) or os.path.getmtime(x) > t for x in files + [os.path.abspath(__file__)])
 
 
-def build(force=False, verbose=True, defines=(), tag=""):
+def build(force=False, verbose=True, defines=(), tag="", only=()):
     """defines / tag: a tools-only variant (e.g. defines=("MXA_SEL_SKIP=1",), tag="skip1"
-    -> libmxa_skip1.so, loaded by tools through MXA_LIB); never the product.  Units whose
-    object is up to date (by hipcc's dependency list) are not recompiled unless force."""
+    -> libmxa_skip1.so, loaded by tools through MXA_LIB); never the product.  only: the
+    source files the variant recompiles (the other units link the product's objects, which
+    must be built).  Units whose object is up to date (by hipcc's dependency list) are not
+    recompiled unless force."""
     lib = LIB.replace("libmxa.so", f"libmxa_{tag}.so") if tag else LIB
     if not force and not _stale(lib):
         return lib
     os.makedirs(OBJDIR, exist_ok=True)
     objs, procs = [], []
     for src, suffix, unit_defs in UNITS:  # one hipcc per translation unit, in parallel
+        if tag and only and src not in only:
+            objs.append(os.path.join(OBJDIR, src.replace(".hip", f"{suffix}.o")))
+            continue
         stem = src.replace(".hip", f"{suffix}{'_' + tag if tag else ''}")
         obj, dep = os.path.join(OBJDIR, stem + ".o"), os.path.join(OBJDIR, stem + ".d")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
@@ -102,4 +107,5 @@ def build(force=False, verbose=True, defines=(), tag=""):
 if __name__ == "__main__":
     defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
     tags = [a[6:] for a in sys.argv[1:] if a.startswith("--tag=")]
-    print(build(force="--force" in sys.argv, defines=defs, tag=tags[0] if tags else ""))
+    only = [x for a in sys.argv[1:] if a.startswith("--only=") for x in a[7:].split(",")]
+    print(build(force="--force" in sys.argv, defines=defs, tag=tags[0] if tags else "", only=tuple(only)))

@@ -13,8 +13,9 @@
 //      once, then per 16 output columns ONE v_mfma_i32_16x16x32_i8 (K = 32 = one block: each
 //      block keeps its exact int32 sum), epilogue acc += C * (sP[row][b] * sV[b][d]) in fp32
 //      (P.V is a tolerance-only product); the V^T operands (token-block-major
-//      codes: one contiguous 512-B run per MFMA) straight from HBM / L2, the next block's in
-//      flight while this block's MFMAs run;
+//      codes: one contiguous 512-B run per MFMA) straight from HBM / L2, two blocks ahead
+//      of their MFMAs (the first two issued at the tile's start, in flight through step 1);
+//      the next tile's kept indices loaded during this tile's P.V;
 //   3. the tile's output rows go out; the written code positions are cleared.
 // Every slot runs the same instructions (an unused slot -- k < 4 KS, or a row past the end --
 // scores key 0 and writes its code to a pad column), so the per-slot work has no branches.
@@ -32,8 +33,10 @@ namespace mxa {
 
 constexpr int kFin16 = 16;  // query rows per MFMA tile (one wave)
 constexpr int kFin16Occ = 4;  // waves per SIMD the register allocation aims at
-// (the MFMA B operands, V^T codes, come straight from memory: staged in LDS with the K
-// table they measured 0.214 ms at 3 waves per SIMD against 0.200 ms at 4, DeiT-base)
+// Measured (DeiT-base, same box): the V^T codes staged in LDS per workgroup instead of read
+// from L2: 0.172 vs 0.166 ms (3 workgroups per CU instead of 4; PixArt 0.019 vs 0.021); the
+// next tile's query codes loaded one tile ahead: 0.193 ms (registers).  Phase timing (tools
+// builds): without the V^T loads 0.125 ms, without the score gathers 0.138, neither 0.104.
 
 typedef int v4i16_ __attribute__((ext_vector_type(4)));
 
@@ -51,9 +54,9 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   o += al((size_t)T * kst);
   L.ke = o;
   o += al((size_t)T * nbd * 2);
-  L.vt = o;
   L.ve = o;
   o += al((size_t)ntb * D * 4);
+  L.vt = o;
   L.waves = o;
   L.sp = al((size_t)kFin16 * vst);
   L.bm = L.sp + al((size_t)ntb * kFin16 * 4);
@@ -85,6 +88,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   uint32_t* bmw = reinterpret_cast<uint32_t*>(wb + L.bm);  // [16][ntb]
   const int pr = lane >> 2, ph = lane & 3;  // the lane's tile row and slot phase
 
+  const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
+  uint32_t* bm = bmw + pr * ntb;
+  const int pad = a.tpad + ph;  // an unused slot's code column (never read by the MFMA)
+  const int ln = lane & 15, kg = lane >> 4;
+  const int8_t* vbase = a.vt + (int64_t)bh * D * a.tpad + 8 * kg;
+  constexpr int NDT = 2 * NB;  // 16-column tiles of D <= 32 NB
+  int64_t bv[NDT], bw[NDT];  // V^T operands of key blocks b, b + 1 (in flight ahead of use)
+  auto load_v = [&](int b, int64_t* dst) {
+#pragma unroll
+    for (int u = 0; u < NDT; ++u)
+      if (16 * u < D) dst[u] = *reinterpret_cast<const int64_t*>(vbase + ((int64_t)b * D + min(16 * u + ln, D - 1)) * 32);
+  };
+  // the next tile's kept indices, loaded while the current tile finishes (the query codes are
+  // loaded at the tile's start: one tile ahead they cost more registers than they save)
+  int ixn[KS];
+  auto load_ix = [&](int r0n) {
+    const int rn = r0n + pr;
+    const int64_t gn = (int64_t)bh * a.N + (rn < r_end ? rn : r_beg);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const int s = ph + 4 * t;
+      ixn[t] = rn < r_end && s < k ? kept_get(a, gn * k + s) : 0;
+    }
+  };
+  load_ix(r_beg + kFin16 * wave);  // (in flight through the staging)
+
   // ---- stage the head's K table and V block scales; clear the code tile ---------------
   const int64_t kb = (int64_t)bh * T;
   {
@@ -102,17 +131,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   }
   __syncthreads();
 
-  const int r_beg = (int)blockIdx.y * a.rows_per_wg, r_end = min(a.N, r_beg + a.rows_per_wg);
-  uint32_t* bm = bmw + pr * ntb;
-  const int pad = a.tpad + ph;  // an unused slot's code column (never read by the MFMA)
-  const int ln = lane & 15, kg = lane >> 4;
-  const int8_t* vbase = a.vt + (int64_t)bh * D * a.tpad + 8 * kg;
-  constexpr int NDT = 2 * NB;  // 16-column tiles of D <= 32 NB
   for (int r0 = r_beg + kFin16 * wave; r0 < r_end; r0 += kFin16 * a.waves) {
     const int r = r0 + pr;
     const bool valid = r < r_end;
     const int64_t grow = (int64_t)bh * a.N + (valid ? r : r0);
     const int64_t brow = EXTRA && a.bias ? b_ * a.bs0 + h_ * a.bs1 + (int64_t)(valid ? r : r0) * a.bs2 : -1;
+    // the first two key blocks' V^T operands, in flight through the scores and softmax
+    load_v(0, bv);
+    if (ntb > 1) load_v(1, bw);
     // the row's query codes / exponents and its kept indices
     uint4 qv[2 * NB];
     int qe[NB];
@@ -129,9 +155,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     bool on[KS];
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
-      const int s = ph + 4 * t;
-      on[t] = valid && s < k;
-      ix[t] = on[t] ? kept_get(a, grow * k + s) : 0;
+      on[t] = valid && ph + 4 * t < k;
+      ix[t] = ixn[t];
     }
     auto true_of = [&](int j) -> float {  // true = quantize_elemwise(fl32(QK^T)) * scale (+ bias)
       const float acc = true_dot<NB>(qv, qe, tkc + (size_t)j * kst, tke + j * nbd);
@@ -226,16 +251,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
     float acc[NDT][4];
 #pragma unroll
     for (int u = 0; u < NDT; ++u) acc[u][0] = acc[u][1] = acc[u][2] = acc[u][3] = 0.0f;
-    int64_t bv[NDT];
-    auto load_v = [&](int b, int64_t* dst) {
-#pragma unroll
-      for (int u = 0; u < NDT; ++u)
-        if (16 * u < D) dst[u] = *reinterpret_cast<const int64_t*>(vbase + ((int64_t)b * D + min(16 * u + ln, D - 1)) * 32);
-    };
-    load_v(0, bv);
+    if (r0 + kFin16 * a.waves < r_end) load_ix(r0 + kFin16 * a.waves);
     for (int b = 0; b < ntb; ++b) {
       int64_t bn[NDT];
-      if (b + 1 < ntb) load_v(b + 1, bn);  // the next block's operands in flight
+      if (b + 2 < ntb) load_v(b + 2, bn);  // two blocks ahead
       const int64_t av = *reinterpret_cast<const int64_t*>(ptile + ln * vst + 32 * b + 8 * kg);
       const float4 s4 = *reinterpret_cast<const float4*>(sP + b * kFin16 + 4 * kg);
 #pragma unroll
@@ -251,7 +270,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
         }
       }
 #pragma unroll
-      for (int u = 0; u < NDT; ++u) bv[u] = bn[u];
+      for (int u = 0; u < NDT; ++u) {
+        bv[u] = bw[u];
+        bw[u] = bn[u];
+      }
     }
     // ---- 3. output rows (64-B segments per row); clear the written code positions ---------
 #pragma unroll

@@ -13,4 +13,4 @@ pmc() {  # pmc <dir> <counters...>
 pmc ${T}pi1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES || exit $?
 pmc ${T}pi2 SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU || exit $?
 python tools/pmc_summary.py "$O/${T}pi[12]/**/*counter_collection.csv" > $O/${T}_pmc_$cfg.txt || exit $?
-grep -A20 "select" $O/${T}_pmc_$cfg.txt
+cat $O/${T}_pmc_$cfg.txt
