@@ -74,7 +74,7 @@ inline int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; 
 struct AttnLayout {
   int nbd, dpad, ntb, tpad;
   int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail, fbf, mask;
-  int64_t xc, xs, slow;  // fused qkv projection: x codes / exponents, slow-head list
+  int64_t xc, xs;  // fused qkv projection: x codes / exponents
   int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
                               // copy (D % 32 != 0 only), the GEMM's fp64 wave list
   int64_t total;
@@ -148,7 +148,6 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
     const int64_t nbk = (xq->C + 31) / 32, tokens = (int64_t)p->B * p->N;
     L.xc = take(tokens * nbk * 32);
     L.xs = take(tokens * nbk * 2);
-    L.slow = take(4 * (1 + (int64_t)L.ntb * p->B * p->H));  // count, then the entries
   }
   if (pj) {
     const int64_t C = (int64_t)p->H * p->D, nbk = (C + 31) / 32, tokens = (int64_t)p->B * p->N;
@@ -214,10 +213,7 @@ static int launch_qkv_proj(const mxa_attn_params& pp, const mxa_qkv_params& xq, 
   pa.pk_bytes = (int)(W.pe - W.pk);
   pa.pe_bytes = (int)(W.ps - W.pe);
   pa.pd_bytes = (int)(W.total - W.pd);
-  pa.slow_count = reinterpret_cast<int*>(ws + L.slow);
-  pa.slow_list = pa.slow_count + 1;
   pa.ntb = (pp.N + 31) / 32;
-  if (hipMemsetAsync(pa.slow_count, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
   pa.bias = xq.bias; pa.qkv_out = xq.qkv_out;
   pa.autocast = xq.autocast_dtype;
   pa.B = pp.B; pa.N = pp.N; pa.H = pp.H; pa.D = pp.D; pa.nbk = nbk; pa.Cpad = Cpad; pa.bfloat = pp.bfloat;

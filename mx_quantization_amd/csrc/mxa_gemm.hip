@@ -14,7 +14,7 @@ int gemm_smax(int nbk) {
   return s;
 }
 
-// the fp64 kernel's list (count, then tile * 4 + wave entries), then the digit kernel's flag
+// the fp64 kernel's list (count, then tile * 4 + wave entries)
 static int64_t gemm_tiles(int M, int Nc, int64_t batch) {
   return (int64_t)((M + kGemmRows - 1) / kGemmRows) * ((Nc + kGemmCols - 1) / kGemmCols) * batch;
 }
@@ -32,17 +32,14 @@ static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, int* slow, hipStrea
                         reinterpret_cast<const void*>(&mx_gemm_slow_kernel<PLAIN>)})
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
   ga.slow = slow;
-  ga.dig_flag = nullptr;
   if (ga.bpd && batch == 1 && ga.nbk <= kGemmDigNbkMax) {
-    // the exponent-folded digits first; the kernels below then run only if a row block
-    // could not take them
+    // a prepared weight: the exponent-folded digits, every row block in the one launch (a
+    // block the digits cannot take sums its K-blocks in fp64 in the same workgroup)
     const size_t dl = gemm_dig_lds(ga.nbk).total;
     const void* dk = reinterpret_cast<const void*>(&mx_gemm_dig_kernel<PLAIN>);
     if (hipFuncSetAttribute(dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl) != hipSuccess) return MXA_ERR_LAUNCH;
-    ga.dig_flag = slow + 1 + 4 * gemm_tiles(ga.M, ga.Nc, 1);
-    if (hipMemsetAsync(ga.dig_flag, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
     hipLaunchKernelGGL(mx_gemm_dig_kernel<PLAIN>, dim3((unsigned)((ga.M + 31) / 32)), dim3(256), dl, stream, ga);
-    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
+    return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
   }
   // grid.z <= 65535: larger batches in slices (each slice lists its slow waves by its own
   // batch index, so every slice runs its own fp64 pass)

@@ -79,9 +79,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   int* cn = reinterpret_cast<int*>(smem + L.cn);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m0g = tm * kGemmRows, n0g = tn * kGemmCols;
-  if constexpr (!SLOW) {  // every row block already taken by the digit kernel
-    if (a.dig_flag && __builtin_amdgcn_readfirstlane(*a.dig_flag) == 0) return;
-  }
   const int16_t* aeb = a.ae + bat * a.ae_bat;
   const int16_t* beb = a.be + bat * a.be_bat;
 
@@ -370,9 +367,12 @@ __global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
 // four digit products accumulate in the MFMA's own int32 accumulators over all K-blocks
 // (lo x lo; lo x hi + hi x lo; hi x hi: |sum| <= 2 nbk 32 128^2 < 2^31) -- no VALU per
 // block -- so sum = c0 + 2^8 c1 + 2^16 c2 (exact in fp64) rounds once: the same correctly
-// rounded exact product as gemm_tile's shifted int32 sums.  A block whose row spreads or
-// the weight's column spreads exceed kDigitSpread (or whose result could be subnormal)
-// sets a.dig_flag, and the shifted-int32 kernels then run the whole product.
+// rounded exact product as gemm_tile's shifted int32 sums.  A row block whose spreads or
+// the weight's column spreads exceed kDigitSpread (or whose result could be subnormal) is
+// summed here block by block in fp64 instead (the MFMA-ready weight codes, ascending
+// K-blocks: the sums of mx_gemm_slow_kernel, exact while the scaled blocks span <= 34 bits
+// -- so also wherever the shifted int32 sums are exact), so one launch covers every row
+// block: no flag, no follow-up kernels.
 struct GemmDigLds {
   size_t ad, rlo, rhi, rn, st, total;
 };
@@ -449,13 +449,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
     glo = wave_reduce(glo, [](uint32_t u, uint32_t w) { return u < w ? u : w; });
     const bool ok = smx <= (uint32_t)kDigitSpread && gsp <= (uint32_t)kDigitSpread &&
                     (lmn == 0xFFFFFFFFu || (int)lmn + (int)glo - (2 << 20) >= -126);
-    if (lane == 0) {
-      st[0] = ok;
-      if (!ok) atomicOr(a.dig_flag, 1);
-    }
+    if (lane == 0) st[0] = ok;
   }
   __syncthreads();
-  if (!st[0]) return;  // uniform over the workgroup
+  const int ncb = (a.Nc + 31) / 32, last = nbk - 1;
+  const int ln = lane & 31, m0 = 4 * (lane >> 5);
+  // out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) for element i of the
+  // lane's 32 x 32 tile of column block cb; value(i, m) the fp32 sum of row m
+  auto store_out = [&](int cb, auto&& value) {
+    const int n = 32 * cb + ln;
+    if (n >= a.Nc) return;
+    const bool cnan = a.bpn[n] != 0;
+    const float bb = a.bias ? (PLAIN ? a.bias[n] : round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1)) : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 8 * (i >> 2) + m0 + (i & 3);
+      if (m >= rows) continue;
+      float o = (cnan || rn[m]) ? __uint_as_float(0x7FC00000u) : value(i, m);
+      if constexpr (PLAIN) {
+        o = a.bias ? o + bb : o;
+      } else {
+        // autocast: F.linear returns the dtype, then the output rounding, then + fp32 bias
+        o = round_bfloat(round_dt(o, a.autocast), a.bfloat, kRoundNearest, 1, a.autocast);
+        if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
+      }
+      static_cast<float*>(a.c)[(int64_t)(m0g + m) * a.ldc + n] = o;
+    }
+  };
+  if (!st[0]) {  // (uniform over the workgroup) the fp64 block sums
+    const v16i_g zero = {};
+    for (int cb = wave; cb < ncb; cb += 4) {
+      const int8_t* bp = a.bpk + ((int64_t)min(cb, a.b_nb32 - 1) * nbk * 64 + lane) * 16;
+      const int n = min(32 * cb + ln, a.Nc - 1);
+      double acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+      for (int kb = 0; kb < nbk; ++kb) {
+        const v4i_g av = *reinterpret_cast<const v4i_g*>(code_at(min(ln, rows - 1), kb, lane >> 5));
+        const v4i_g bv = *reinterpret_cast<const v4i_g*>(bp + (int64_t)kb * 1024);
+        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, zero, 0, 0, 0);
+        const int eb = exp_from16(a.be[(int64_t)n * a.be_n + (int64_t)kb * a.be_k]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = min(8 * (i >> 2) + m0 + (i & 3), rows - 1);
+          const int ea = exp_at(m, kb);
+          // a NaN block: the row / column flag makes the output NaN; its term adds 0 here
+          acc[i] += (ea == kExpNaN || eb == kExpNaN) ? 0.0 : ldexp((double)c[i], ea + eb);
+        }
+      }
+      store_out(cb, [&](int i, int) { return (float)acc[i]; });
+    }
+    return;
+  }
 
   // ---- the rows' digits: chunk (kb, lane) = row lane % 32, half lane / 32 ----------------
   for (int i = tid; i < 64 * nbk; i += 256) {
@@ -475,8 +520,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
   __syncthreads();
 
   // ---- per wave: 32-column blocks wave, wave + 4, ... --------------------------------
-  const int ncb = (a.Nc + 31) / 32, last = nbk - 1;
-  const int ln = lane & 31, m0 = 4 * (lane >> 5);
   const int8_t* adl = ad + lane * 16;
   auto cl = [&](int kb) { return min(kb, last); };
   for (int cb = wave; cb < ncb; cb += 4) {
@@ -506,29 +549,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
     if (kb < nbk) step(kb, L0, H0);
     if (kb + 1 < nbk) step(kb + 1, L1, H1);
     if (kb + 2 < nbk) step(kb + 2, L2, H2);
-    // ---- out = bf(fl32(sum)); out = bf(out + bf(bias))  (linear.py:88-101) ---------------
-    const int n = 32 * cb + ln;
-    if (n < a.Nc) {
-      const int clo = a.bps[2 * n];
-      const bool cnan = a.bpn[n] != 0;
-      const float bb = a.bias ? (PLAIN ? a.bias[n] : round_bfloat(a.bias[n], a.bfloat, kRoundNearest, 1)) : 0.0f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = 8 * (i >> 2) + m0 + (i & 3);
-        if (m >= rows) continue;
-        const int lo = rlo[m] > rhi[m] ? 0 : rlo[m];
-        const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
-        float o = (cnan || rn[m]) ? __uint_as_float(0x7FC00000u) : (float)ldexp(v, lo + clo);
-        if constexpr (PLAIN) {
-          o = a.bias ? o + bb : o;
-        } else {
-          // autocast: F.linear returns the dtype, then the output rounding, then + fp32 bias
-          o = round_bfloat(round_dt(o, a.autocast), a.bfloat, kRoundNearest, 1, a.autocast);
-          if (a.bias) o = round_bfloat(o + bb, a.bfloat, kRoundNearest, 1);
-        }
-        static_cast<float*>(a.c)[(int64_t)(m0g + m) * a.ldc + n] = o;
-      }
-    }
+    const int clo = a.bps[2 * min(32 * cb + ln, a.Nc - 1)];
+    store_out(cb, [&](int i, int m) {
+      const int lo = rlo[m] > rhi[m] ? 0 : rlo[m];
+      const double v = (double)c0[i] + 256.0 * (double)c1[i] + 65536.0 * (double)c2[i];
+      return (float)ldexp(v, lo + clo);
+    });
   }
 }
 

@@ -158,15 +158,6 @@ static int launch_proj_nbd(const ProjArgs& pa, hipStream_t stream) {
   const int ng = (pa.H + p.hpg - 1) / p.hpg;
   hipLaunchKernelGGL((qkv_proj_kernel<NBD, PLAIN>), dim3((unsigned)((pa.N + 31) / 32), (unsigned)pa.B, (unsigned)ng),
                      dim3(64 * 3 * NBD), lds, stream, p);
-  if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
-  // the heads listed for the fp64 block sums (usually none: every workgroup reads the
-  // count and leaves)
-  const void* slow = reinterpret_cast<const void*>(&qkv_proj_slow_kernel<NBD, PLAIN>);
-  if (hipFuncSetAttribute(slow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
-  const int64_t entries = (int64_t)pa.ntb * pa.B * pa.H;
-  const unsigned sgrid = (unsigned)std::min<int64_t>(entries, (int64_t)cus);
-  hipLaunchKernelGGL((qkv_proj_slow_kernel<NBD, PLAIN>), dim3(sgrid), dim3(64 * 3 * NBD), lds, stream, p);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 

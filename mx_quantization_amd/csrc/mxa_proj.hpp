@@ -72,10 +72,9 @@ __host__ __device__ inline ProjLds proj_lds(int Cpad, int nbk, int D) {
 // PLAIN (proj_plain): no bfloat rounding, no flush, no autocast, q / k operands of
 // rows_prep_block_plain and V's MXINT8 -- the bench path, compiled without the general
 // rounding code (a third of the code and registers of the general instantiation).
-// SLOW: the block sums in fp64 (qkv_proj_slow_kernel); else in shifted int32, and a head
-// whose exponent spreads do not allow that is listed for the slow kernel -- so the
-// common kernel carries no fp64 code and no registers for it.
-template <int NBD, bool PLAIN, bool SLOW>
+// Per head: the exponent-folded digits, the shifted int32 block sums, or (wide spreads, a
+// subnormal result) fp64 block sums, all in this workgroup.
+template <int NBD, bool PLAIN>
 __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int h_begin, int h_end,
                                            unsigned char* smem) {
   constexpr int kThreads = 64 * 3 * NBD;
@@ -171,11 +170,11 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     if (lane == 0) {
       st[0] = (int)smx;
       st[1] = (int)bmn - (1 << 20);
-      st[2] = !SLOW && smx <= kDigitSpread && gmx <= kDigitSpread;
+      st[2] = smx <= kDigitSpread && gmx <= kDigitSpread;
     }
   }
   __syncthreads();
-  const bool dig = !SLOW && st[2];  // uniform over the workgroup
+  const bool dig = st[2];  // uniform over the workgroup
   int8_t* xh = reinterpret_cast<int8_t*>(smem + L.xh);
   auto put_code = [&](int i, const uint4& v) {
     const int m = i / cpr, c = i - m * cpr;
@@ -226,12 +225,13 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
     // row and column exponent spreads sum to <= smax, the block sums shifted by
     // (ex - rowmin) + (ew - colmin) add up exactly in int32, and one conversion gives
     // the correctly rounded result (2 VALU per element and block).  Otherwise (or when
-    // the result could be subnormal) the blocks are summed in fp64 by the slow kernel:
+    // the result could be subnormal) the blocks are summed in fp64 (run_f64, below):
     // exact while their scaled exponents span <= 34 bits, within fp32 rounding beyond.
     // The decision is per head (the largest column spread of its q, k, v weight groups,
     // uniform over the workgroup).  A workgroup whose row spreads and heads' column spreads
     // are all <= kDigitSpread takes the exponent-folded operands instead (run_dig below).
-    if constexpr (!SLOW) {
+    bool fast_ok;
+    {
       int gsp = 0, glo = 1 << 20;
 #pragma unroll
       for (int s3 = 0; s3 < 3; ++s3) {
@@ -240,10 +240,7 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         gsp = max(gsp, (int)a.gs[2 * g + 1]);
       }
       // (the digit path's sums are exact at any spread it takes: only the subnormal test)
-      if (!((dig || st[0] + gsp <= a.smax) && st[1] + glo >= -126)) {
-        if (threadIdx.x == 0) a.slow_list[atomicAdd(a.slow_count, 1)] = (b * a.ntb + tb) * a.H + h;
-        continue;  // uniform over the workgroup
-      }
+      fast_ok = (dig || st[0] + gsp <= a.smax) && st[1] + glo >= -126;  // uniform over the workgroup
     }
     const int64_t jcol = (int64_t)s * HD + (int64_t)h * D + dcol;
     const float bb = (a.bias && colv) ? (PLAIN ? a.bias[jcol] : round_bfloat(a.bias[jcol], a.bfloat, kRoundNearest, 1)) : 0.0f;
@@ -273,11 +270,11 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
         }
       }
     };
-    // the K loop and the epilogue, specialised on the accumulation (FAST: shifted int32;
-    // else fp64): separate live ranges, so the two never hold registers together
+    // the K loop and the epilogue of the shifted int32 sums (FAST; the fp64 form: run_f64)
     auto run = [&](auto fast_c) {
       constexpr bool FAST = decltype(fast_c)::value;
-      typename std::conditional<FAST, int, double>::type acc[16];
+      static_assert(FAST, "the fp64 sums: run_f64");
+      int acc[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0;
       // Software pipeline over the K-blocks, unrolled by four so that every operand is
@@ -426,9 +423,41 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
           },
           a.pn[pc] != 0);
     };
+    // the fp64 block sums for a head whose spreads allow neither the digits nor the shifted
+    // int32 sums (rare): one K-block at a time, ascending (exact while the scaled blocks span
+    // <= 34 bits, within fp32 rounding beyond) -- few registers, so the common paths keep theirs
+    auto run_f64 = [&]() {
+      double acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+      const v16i zero = {};
+      // (a digit tile -- its subnormal test failed -- holds code * 2^xe as two base-256 digits:
+      // the block's sum c0 + 256 c1 is then the shifted sum, scaled by the row's base exponent)
+      const int8_t* xha = reinterpret_cast<int8_t*>(smem + L.xh) + ln * L.xst + kh;
+      for (int kb = 0; kb < nbk; ++kb) {
+        const v4i_ w = __builtin_bit_cast(v4i_, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff, wsoff + kb * 1024, 0));
+        v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_*>(xa + 32 * kb), w, zero, 0, 0, 0);
+        if (dig) {
+          const v16i ch = __builtin_amdgcn_mfma_i32_32x32x32_i8(*reinterpret_cast<const v4i_*>(xha + 32 * kb), w, zero, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) c[i] += ch[i] << 8;
+        }
+        int ew = exp_from16((int16_t)__builtin_amdgcn_raw_buffer_load_b16(ers, eoff, esoff + kb * 2, 0));
+        cnan = cnan || ew == kExpNaN;
+        ew = ew == kExpNaN ? wlo : ew;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = 8 * (i >> 2) + m0 + (i & 3);
+          const int base = dig ? (rlo[m] > rhi[m] ? 0 : rlo[m]) : (int)xe[kb * 32 + m] + rlo[m];
+          acc[i] += ldexp((double)c[i], base + ew);
+        }
+      }
+      store_tile([&](int i, int) { return (float)acc[i]; }, cnan);
+    };
     if (MXA_PROJ_SKIP & 1) store_tile([](int, int) { return 0.0f; }, false);
-    else if (dig) run_dig();
-    else run(std::integral_constant<bool, !SLOW>{});
+    else if (fast_ok && dig) run_dig();
+    else if (fast_ok) run(std::true_type{});
+    else run_f64();  // wide spreads or a subnormal result: fp64, in this workgroup
 
     __syncthreads();
     if (a.qkv_out) {  // the fp32 projection (tests): whole rows of the tile, coalesced
@@ -486,22 +515,8 @@ __device__ __forceinline__ void proj_block(const ProjArgs& a, int tb, int b, int
 template <int NBD, bool PLAIN>
 __global__ __launch_bounds__(64 * 3 * NBD) __attribute__((amdgpu_waves_per_eu(4, 8))) void qkv_proj_kernel(ProjArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  proj_block<NBD, PLAIN, false>(a, blockIdx.x, blockIdx.y, (int)blockIdx.z * a.hpg,
+  proj_block<NBD, PLAIN>(a, blockIdx.x, blockIdx.y, (int)blockIdx.z * a.hpg,
                                 min(a.H, ((int)blockIdx.z + 1) * a.hpg), smem);
-}
-
-// the (token block, image, head) tiles qkv_proj_kernel listed: a fixed grid strides over
-// the list (its length is known on the device only; an empty list costs one read)
-template <int NBD, bool PLAIN>
-__global__ __launch_bounds__(64 * 3 * NBD) void qkv_proj_slow_kernel(ProjArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int n = __builtin_amdgcn_readfirstlane(*a.slow_count);
-  for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    const int e = __builtin_amdgcn_readfirstlane(a.slow_list[i]);
-    const int h = e % a.H, t = e / a.H;
-    proj_block<NBD, PLAIN, true>(a, t % a.ntb, t / a.ntb, h, h + 1, smem);
-    __syncthreads();  // the next entry restages the LDS tile
-  }
 }
 
 }  // namespace mxa

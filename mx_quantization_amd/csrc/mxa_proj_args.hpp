@@ -97,8 +97,6 @@ struct ProjArgs {
   const int16_t* gs;  // per weight group: smallest exponent, largest spread (the head's fast-path test)
   const int16_t* pn;  // per padded column: NaN block flag
   const int8_t* pd;   // exponent-folded digit codes
-  int* slow_count;    // heads listed for qkv_proj_slow_kernel (zeroed before the launch)
-  int* slow_list;     // (b * ntb + tb) * H + h
   const float* bias;  // [3*H*D] or null
   float* qkv_out;     // optional [B*N][3*H*D] projection (tests)
   int B, N, H, D, nbk, Cpad, bfloat, ntb;
@@ -136,9 +134,6 @@ struct GemmArgs {
   const int8_t* bpd;
   const int16_t *bps, *bpn, *bgs;
   int bG;
-  // set (non-zero) by mx_gemm_dig_kernel when a row block could not take the digits: the
-  // shifted-int32 kernels then run the whole product; null = no digit kernel ran
-  int* dig_flag;
 };
 
 }  // namespace mxa
