@@ -143,11 +143,8 @@ static int launch_finish(const Rows2Args& ra, int BH, hipStream_t stream, bool p
   const int kind = rows_kernel_kind(true, ra.k_top, ra.T, ra.nbd, ra.xo_codes != nullptr);
   const bool xdt = ra.s_dt != kF32 || ra.in_dt != kF32;
   if (kind == MXA_FIN_MFMA) return xdt ? launch_finish_qk_x1(ra, BH, stream, plan) : launch_finish_qk_x0(ra, BH, stream, plan);
-  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k with
-  // T > 256: the 32-row kernel.  The proj's MX input codes (XO) stay on the 32-row kernel:
-  // its 32 x 32 output blocks are whole MX blocks of the output rows (measured: 0.264 ms at
-  // DeiT-base against 0.308 ms for 16-row tiles, whose 16 x 32 blocks take twice the
-  // transposes and syncs per row).
+  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row (also with the
+  // proj's MX input codes for k <= 32); larger k with T > 256: the 32-row kernel.
   if (kind == MXA_FIN_GATHER16) return xdt ? launch_finish16_x1(ra, BH, stream, plan) : launch_finish16_x0(ra, BH, stream, plan);
   switch (ra.nbd) {
     case 1: return launch_finish32_p1(ra, BH, stream, plan);

@@ -26,7 +26,8 @@ constexpr bool kF16Xdt = MXA_F16_XDT != 0;
 // over its tiles (a head's tiles round-robin over the waves: the K table staged once)
 static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, int* waves, int* rows_per_wg) {
   const int tiles = (ra.N + kFin16 - 1) / kFin16;
-  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w).total; };
+  const bool xo = ra.xo_codes != nullptr;
+  auto lds = [&](int w) { return fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, w, xo).total; };
   if (lds(1) > 160 * 1024) return MXA_ERR_UNSUPPORTED;
   int chunks = 1;
   while ((int64_t)BH * chunks < 512 && chunks < tiles) ++chunks;
@@ -46,10 +47,10 @@ static int finish16_plan(const Rows2Args& ra, int BH, int regs_waves_per_simd, i
   *rows_per_wg = kFin16 * ((tiles + chunks - 1) / chunks);
   return MXA_OK;
 }
-template <int NB, int KS, bool EXTRA>
+template <int NB, int KS, bool EXTRA, bool XO = false>
 static int launch_finish16_x(const Rows2Args& ra0, int BH, hipStream_t stream) {
   Rows2Args ra = ra0;
-  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, kF16Xdt, EXTRA>);
+  const void* fn = reinterpret_cast<const void*>(&finish16_kernel<NB, KS, kF16Xdt, EXTRA, XO>);
   // waves per SIMD the kernel's registers allow: a property of the code object (gfx950
   // only), cached per instantiation; concurrent first launches compute the same value
   static std::atomic<int> regs_wps{0};
@@ -61,18 +62,25 @@ static int launch_finish16_x(const Rows2Args& ra0, int BH, hipStream_t stream) {
   }
   int rc = finish16_plan(ra, BH, wps, &ra.waves, &ra.rows_per_wg);
   if (rc) return rc;
-  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves).total;
+  const size_t lds = fin16_lds(ra.T, ra.D, ra.kst, ra.nbd, ra.vst, ra.ntb, ra.waves, XO).total;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return MXA_ERR_LAUNCH;
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
-  hipLaunchKernelGGL((finish16_kernel<NB, KS, kF16Xdt, EXTRA>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds, stream,
-                     ra);
+  hipLaunchKernelGGL((finish16_kernel<NB, KS, kF16Xdt, EXTRA, XO>), dim3((unsigned)BH, gy), dim3(64 * ra.waves), lds,
+                     stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
 }
 template <int NB, int KS>
 static int launch_finish16_ks(const Rows2Args& ra, int BH, hipStream_t stream) {
   // EXTRA: a bias, the debug true scores or bfloatX rounding (float16 / bfloat16 always round)
   const bool extra = kF16Xdt || ra.bias || ra.true_out || (ra.bfloat != 0 && ra.bfloat != 32);
+  if (ra.xo_codes) {  // the proj Linear's MX input codes: float32, D % 32 == 0, k <= 32
+    if constexpr (!kF16Xdt && KS <= 8) {
+      if (ra.D % 32) return MXA_ERR_UNSUPPORTED;
+      return extra ? launch_finish16_x<NB, KS, true, true>(ra, BH, stream) : launch_finish16_x<NB, KS, false, true>(ra, BH, stream);
+    }
+    return MXA_ERR_UNSUPPORTED;
+  }
   if (extra) return launch_finish16_x<NB, KS, true>(ra, BH, stream);
   if constexpr (!kF16Xdt) return launch_finish16_x<NB, KS, false>(ra, BH, stream);
   return MXA_ERR_UNSUPPORTED;
@@ -89,7 +97,7 @@ static int launch_finish16_nb(const Rows2Args& ra, int BH, hipStream_t stream) {
 }
 
 int MXA_F16_FN(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
-  if (ra.xo_codes) return MXA_ERR_UNSUPPORTED;  // the proj's input codes: the 32-row kernel
+  if (ra.xo_codes && (kF16Xdt || ra.k_top > 32 || ra.D % 32)) return MXA_ERR_UNSUPPORTED;
   if (plan) {
     int w, r;
     return ra.k_top <= 64 ? finish16_plan(ra, BH, 2, &w, &r) : MXA_ERR_UNSUPPORTED;

@@ -46,7 +46,10 @@ typedef int v4i16_ __attribute__((ext_vector_type(4)));
 struct Fin16Lds {
   size_t kc, ke, vt, ve, waves, per_wave, sp, bm, total;
 };
-__host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves) {
+// xo: the per-wave area also holds the 16 x (D + 1) fp32 output tile being MX-quantized for
+// the proj Linear (over the code tile, sP and bm, which are rewritten afterwards)
+__host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, int vst, int ntb, int waves,
+                                              bool xo = false) {
   Fin16Lds L;
   size_t o = 0;
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -61,14 +64,18 @@ __host__ __device__ inline Fin16Lds fin16_lds(int T, int D, int kst, int nbd, in
   L.sp = al((size_t)kFin16 * vst);
   L.bm = L.sp + al((size_t)ntb * kFin16 * 4);
   L.per_wave = L.bm + al((size_t)kFin16 * ntb * 4);
+  if (xo && L.per_wave < al((size_t)kFin16 * (D + 1) * 4)) L.per_wave = al((size_t)kFin16 * (D + 1) * 4);
   L.total = o + (size_t)waves * L.per_wave;
   return L;
 }
 
 // NB: 32-blocks per head dim; KS: kept slots per lane (k <= 4 KS); XDT: float16 / bfloat16
 // inputs or scores (the dtype roundings at run time); EXTRA: a bias, the debug true-score
-// output or bfloatX rounding (else the scores and P are plain float32)
-template <int NB, int KS, bool XDT, bool EXTRA>
+// output or bfloatX rounding (else the scores and P are plain float32); XO: the output rows
+// go to the proj Linear as MX codes along C (Rows2Args::xo_codes; float32, D % 32 == 0):
+// the tile's 16 x D block is transposed through LDS and every 32-column block of every row
+// quantized by rows_prep's per-block body (two lanes per block, all 64 lanes for D = 64)
+template <int NB, int KS, bool XDT, bool EXTRA, bool XO = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && KS <= 12 ? kFin16Occ : (NB * KS <= 64 ? 3 : 2), 8))) void finish16_kernel(Rows2Args a) {
   constexpr bool kRound = XDT || EXTRA;
   const int sdt = XDT ? a.s_dt : (int)kF32, idt = XDT ? a.in_dt : (int)kF32;
@@ -78,7 +85,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
   const int T = a.T, D = a.D, kst = a.kst, vst = a.vst, ntb = a.ntb, k = a.k_top;
   constexpr int nbd = NB;
   const int b_ = bh / a.H, h_ = bh % a.H;
-  const Fin16Lds L = fin16_lds(T, D, kst, nbd, vst, ntb, a.waves);
+  const Fin16Lds L = fin16_lds(T, D, kst, nbd, vst, ntb, a.waves, XO);
   int8_t* tkc = reinterpret_cast<int8_t*>(smem + L.kc);
   int16_t* tke = reinterpret_cast<int16_t*>(smem + L.ke);
   float* tvs = reinterpret_cast<float*>(smem + L.ve);
@@ -274,6 +281,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB <= 2 && 
         bv[u] = bw[u];
         bw[u] = bn[u];
       }
+    }
+    if constexpr (XO) {
+      // ---- 3'. the 16 x D block -> MX codes of blocks h NB .. of each output row (what
+      // rows_prep makes of the (B, N, C) output for the proj Linear: finish_kernel's XO) ------
+      wave_lds_sync();  // every lane's MFMA reads of the code tile are done
+      float* ot = reinterpret_cast<float*>(wb);
+      const int ost = D + 1;
+#pragma unroll
+      for (int u = 0; u < NDT; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (16 * u + ln < D) ot[(4 * kg + i) * ost + 16 * u + ln] = round_bfloat(acc[u][i], a.bfloat, kRoundNearest, 1);
+      wave_lds_sync();
+      RowsPrepArgs ro{};
+      ro.codes = a.xo_codes; ro.sT = a.xo_exps;
+      ro.dpad = a.H * D; ro.nb = a.H * nbd; ro.D = a.H * D;
+      ro.op_kind = MXA_OP_MXINT8; ro.flush = a.flush_p; ro.bfloat = a.bfloat; ro.dt = kF32;
+      ro.mfma_rows = 1;  // the MX GEMM's A layout
+      const int row = (lane & 31) >> 1, sub = lane & 1, rr = r0 + row;
+      const int64_t orow = (int64_t)b_ * a.N + (rr < r_end ? rr : r0);
+#pragma unroll
+      for (int bp = 0; bp < NB; bp += 2) {
+        const int bl = bp + (lane >> 5), blc = min(bl, NB - 1);
+        float xv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) xv[j] = ot[row * ost + 32 * blc + 16 * sub + j];
+        const int blk = h_ * nbd + blc, c0 = h_ * D + 32 * blc + 16 * sub;
+        if (rows_prep_plain(ro)) rows_prep_block_plain<16, kF32>(ro, orow, blk, sub, c0, xv, rr < r_end && bl < NB);
+        else rows_prep_block<16>(ro, orow, blk, sub, c0, xv, rr < r_end && bl < NB);
+      }
+      wave_lds_sync();
+      // the area back to a clear code tile and zero block maxima (sP is rewritten per tile)
+      for (int i = lane; i < (int)(L.per_wave / 16); i += 64) reinterpret_cast<uint4*>(wb)[i] = make_uint4(0, 0, 0, 0);
+      wave_lds_sync();
+      continue;
     }
     // ---- 3. output rows (64-B segments per row); clear the written code positions ---------
 #pragma unroll

@@ -62,10 +62,9 @@ inline bool finish_qk_dense_ok(int T, int nbd) { return T <= 256 && nbd <= 4; }
 inline int rows_kernel_kind(bool topk, int k, int T, int nbd, bool xo) {
   if (!topk) return finish_qk_dense_ok(T, nbd) ? MXA_FIN_DENSE_MFMA : MXA_FIN_DENSE_ROWS;
   if (finish_qk_wanted(k, T, nbd, xo)) return MXA_FIN_MFMA;
-  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row; larger k, and
-  // the proj's MX input codes (32 x 32 output tiles = whole MX blocks of the output rows):
-  // the 32-row kernel
-  return k <= 64 && !xo ? MXA_FIN_GATHER16 : MXA_FIN_GATHER32;
+  // k <= 64 (DeiT's 20 / 30, PixArt's 20): 16-row tiles, four lanes per row (with the proj's
+  // MX input codes: k <= 32); larger k: the 32-row kernel
+  return k <= (xo ? 32 : 64) ? MXA_FIN_GATHER16 : MXA_FIN_GATHER32;
 }
 // its launches (mxa_fin_qk.hip): float32 inputs and scores (x0), float16 / bfloat16 (x1)
 int launch_finish_qk_x0(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);
