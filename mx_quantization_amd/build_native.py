@@ -26,7 +26,7 @@ UNITS += [("mxa_proj.hip", "", ()), ("mxa_gemm.hip", "", ())]
 UNITS += [("mxa_fin_qk.hip", f"_x{i}", (f"MXA_FQ_XDT={i}",)) for i in range(2)]
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["mxa_common.hpp", "mxa_kernels.hpp", "mxa_prep.hpp", "mxa_proj.hpp", "mxa_proj_args.hpp", "mxa_finish.hpp",
-           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_finish16.hpp", "mxa_finish_qk.hpp", "mxa_tail.hpp", "mxa_gemm.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
+           "mxa_order.hpp", "mxa_topk_grp.hpp", "mxa_topk_wave.hpp", "mxa_finish16.hpp", "mxa_finish_qk.hpp", "mxa_tail.hpp", "mxa_gemm.hpp", "mxa_dot.hpp", "mxa_select.hpp", "mxa_rows2.hpp", "mxa_modes.hpp", "mxa_launch.hpp",
            "../../include/mxa.h"]
 ARCH = os.environ.get("MXA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -23,7 +23,7 @@
 // workloads/PixArt/models/MX_transformer_block.py:679-717, :826-859.
 #pragma once
 #include "mxa_prep.hpp"
-#include "mxa_select.hpp"
+#include "mxa_dot.hpp"
 
 namespace mxa {
 

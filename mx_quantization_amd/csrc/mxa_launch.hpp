@@ -10,9 +10,15 @@ inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr
 
 // selection kernel (mxa_sel.hip); plan: only check the LDS budget, launch nothing
 int launch_select(const Rows2Args& ra, int mode, int BH, hipStream_t stream, bool plan);
-// the one-lane tail's prefix (measured: a 32-position prefix for k <= 30 is no faster -- the
-// selection kernel then runs one more lockstep step per row)
-constexpr int kTailPref = 64;
+// the one-lane tail's prefix (measured, DeiT-base: 48 positions 0.575-0.583 ms against 0.585-0.599
+// for 64 -- 12 KB of LDS per wave, 3 waves per SIMD instead of 2, outweighs the selection kernel's
+// extra step -- and 0.573-0.584 for 56; a 32-position prefix is slower: the selection kernel then
+// runs one more lockstep step per row).  MXA_TAIL_PREF: a tools-only
+// build of another width for same-box A/Bs (build_native defines)
+#ifndef MXA_TAIL_PREF
+#define MXA_TAIL_PREF 48
+#endif
+constexpr int kTailPref = MXA_TAIL_PREF;
 // the selection's packed pass: rows of <= 256 keys, the approximators whose scores pack
 // (sums of a few small integers times powers of two), no bias (a bias of -10000 next to
 // small scores needs the key's low byte: PixArt's masked cross-attention would fall back
@@ -22,12 +28,13 @@ inline bool sel_packs(int mode, int T, bool bias) {
 }
 // the prefix the one-lane tail takes over (mxa_tail.hpp), 0 = none: k + 2 <= TW (the
 // introselect's last range and the sort of [0, k-1) lie in it), not partial_sort (k*64 <= T)
-// (k - 1 <= 32: the final stable rank of [0, k-1) in at most 32 registers per lane)
-inline int sel_tail_width(int mode, int T, int k, bool bias) {
-  if (!sel_packs(mode, T, bias) || k <= 0 || k > 33 || (int64_t)k * 64 <= T) return 0;
-  if (k + 2 <= kTailPref) return kTailPref;
-  return k + 2 <= 64 ? 64 : 0;
+// (k - 1 <= 32: the final stable rank of [0, k-1) in at most 32 registers per lane; k + ntw
+// <= TW: the prune-mask words are set in the prefix's free positions)
+inline int tail_width_for(int n, int k) {
+  if (k <= 0 || k > 33 || (int64_t)k * 64 <= n) return 0;
+  return k + 2 <= kTailPref && k + (n + 31) / 32 <= kTailPref ? kTailPref : 0;
 }
+inline int sel_tail_width(int mode, int T, int k, bool bias) { return sel_packs(mode, T, bias) ? tail_width_for(T, k) : 0; }
 
 // one score mode per translation unit of mxa_sel.hip (MXA_SEL_PART 1..6)
 int launch_select_p1(const Rows2Args& ra, int BH, hipStream_t stream, bool plan);  // ex_pred

@@ -54,10 +54,9 @@ template <int NP, int MODE, int W>
 static int launch_select_packed(const Rows2Args& ra, int BH, hipStream_t stream, bool plan) {
   const int tw = sel_tail_width(MODE, ra.T, ra.k_top, ra.bias != nullptr);
   int rc;
-  static_assert(kTailPref == 64, "the one-lane tail is instantiated for a 64-position prefix");
-  if (tw == 64) {
-    rc = launch_select_w<NP, MODE, W, uint32_t, 1, 64>(ra, BH, stream, plan);
-    if (rc == MXA_OK) rc = launch_tail<64>(ra, BH, stream, plan);
+  if (tw == kTailPref) {
+    rc = launch_select_w<NP, MODE, W, uint32_t, 1, kTailPref>(ra, BH, stream, plan);
+    if (rc == MXA_OK) rc = launch_tail<kTailPref>(ra, BH, stream, plan);
   } else {
     rc = launch_select_w<NP, MODE, W, uint32_t, 0, 0>(ra, BH, stream, plan);
   }
@@ -134,11 +133,7 @@ static int launch_topk_grp(const GrpTopkArgs& ga, const TopkWs& w, unsigned grid
 // the workspace path of the standalone top-k: the packed pass for rows of <= 256 values
 // (mxa_select.hpp topk_rows16), the one-lane tail for k <= 33 (mxa_tail.hpp), the 64-bit
 // pass over the rows it leaves
-static int topk_ws_tw(int n, int k) {
-  if (k <= 0 || k > 33 || (int64_t)k * 64 <= n) return 0;
-  if (k + 2 <= kTailPref) return kTailPref;
-  return k + 2 <= 64 ? 64 : 0;
-}
+static int topk_ws_tw(int n, int k) { return tail_width_for(n, k); }
 static bool topk_ws_packs(int n, int k) { return n <= 256 && k > 0; }
 static int64_t topk_ws_bytes(int64_t rows, int n, int k) {
   if (!topk_ws_packs(n, k)) return 0;
@@ -219,10 +214,10 @@ extern "C" int mxa_topk_ws(const void* vals, int64_t rows, int32_t n, int64_t ld
   const unsigned grid = (unsigned)w.n_wg;
   const int tw = topk_ws_tw(n, k);
   if (n <= 128) {
-    if (tw == 64) return launch_topk_packed<128, 64>(ga, w, grid, stream);
+    if (tw == kTailPref) return launch_topk_packed<128, kTailPref>(ga, w, grid, stream);
     return launch_topk_packed<128, 0>(ga, w, grid, stream);
   }
-  if (tw == 64) return launch_topk_packed<256, 64>(ga, w, grid, stream);
+  if (tw == kTailPref) return launch_topk_packed<256, kTailPref>(ga, w, grid, stream);
   return launch_topk_packed<256, 0>(ga, w, grid, stream);
 }
 

@@ -22,6 +22,7 @@
 //   workloads/PixArt/models/MX_transformer_block.py:656-678, :805-825.
 #pragma once
 #include <type_traits>
+#include "mxa_dot.hpp"
 #include "mxa_rows2.hpp"
 #include "mxa_topk_grp.hpp"
 #include "mxa_tail.hpp"
@@ -30,8 +31,18 @@
 namespace mxa {
 
 constexpr int kSelRows = 32;   // query rows per workgroup (a multiple of 4 * waves)
-constexpr int kSelOcc = 4;     // waves per SIMD the 64-bit pass is compiled for (rows <= 256 keys)
-constexpr int kSelPOcc = 5;    // ... and the packed pass
+#ifndef MXA_SEL_OCC
+#define MXA_SEL_OCC 4  // (a tools-only build of another occupancy target for same-box A/Bs)
+#endif
+constexpr int kSelOcc = MXA_SEL_OCC;  // waves per SIMD the 64-bit pass is compiled for (rows <= 256 keys)
+#ifndef MXA_SEL_POCC
+#define MXA_SEL_POCC 5  // (a tools-only build of another occupancy target for same-box A/Bs)
+#endif
+constexpr int kSelPOcc = MXA_SEL_POCC;  // ... and the packed pass
+#ifndef MXA_SEL_POCC_NT
+#define MXA_SEL_POCC_NT 5
+#endif
+constexpr int kSelPOccNT = MXA_SEL_POCC_NT;  // ... the packed pass without the tail (k > 33: DiT)
 constexpr int kSelShortT = 224;
 // waves per workgroup: 2 for rows of <= 224 keys on a large grid (DeiT-base: 0.97 ->
 // 0.93 ms), else 4 (DiT: 1.44 vs 1.56 ms with 2; PixArt's 128 heads: 0.069 vs 0.10 ms)
@@ -69,19 +80,6 @@ __host__ __device__ inline SelLds sel_lds(int mode, int T, int D, int kst, int n
   if (mode == kModeExSign) o += 16 * 4;
   L.rows = o;
   return L;
-}
-
-__device__ __forceinline__ int dot32(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
-  int I = 0;
-  I = __builtin_amdgcn_sdot4((int)a0.x, (int)b0.x, I, false);
-  I = __builtin_amdgcn_sdot4((int)a0.y, (int)b0.y, I, false);
-  I = __builtin_amdgcn_sdot4((int)a0.z, (int)b0.z, I, false);
-  I = __builtin_amdgcn_sdot4((int)a0.w, (int)b0.w, I, false);
-  I = __builtin_amdgcn_sdot4((int)a1.x, (int)b1.x, I, false);
-  I = __builtin_amdgcn_sdot4((int)a1.y, (int)b1.y, I, false);
-  I = __builtin_amdgcn_sdot4((int)a1.z, (int)b1.z, I, false);
-  I = __builtin_amdgcn_sdot4((int)a1.w, (int)b1.w, I, false);
-  return I;
 }
 
 // ex_pred score of one key: sum_b m_b 2^(eq_b + ek_b), m_b = n_b - 2 popc(sq_b ^ sk_b)
@@ -137,41 +135,6 @@ __device__ __forceinline__ double g_dot(const uint4* qv, const int* qe, int nbd,
     }
   }
   return acc;
-}
-
-// The true score fl32(sum_b I_b 2^(qe_b + ke_b)) of a query row (codes in registers)
-// and a key row of the LDS code table (MXINT8, exponents in code units): block sums by
-// v_dot4; when the block exponents span <= 10 bits (NB x 2^19 x 2^10 < 2^31) and the
-// smallest is >= -100, the sum shifted to the smallest exponent is an exact int32 and
-// one conversion + exact scaling gives the correctly rounded float (no fp64); otherwise
-// the exact fp64 sum (g_dot).  NaN for a NaN block.
-template <int NB>
-__device__ __forceinline__ float true_dot(const uint4* qv, const int* qe, const int8_t* krow, const int16_t* kexp) {
-  int I[NB], e[NB];
-  int emin = 1 << 20, emax = -(1 << 20);
-  bool nan = false;
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const uint4 x0 = *reinterpret_cast<const uint4*>(krow + 32 * b);
-    const uint4 x1 = *reinterpret_cast<const uint4*>(krow + 32 * b + 16);
-    I[b] = dot32(qv[2 * b], qv[2 * b + 1], x0, x1);
-    const int ke = exp_from16(kexp[b]);
-    nan = nan || ke == kExpNaN || qe[b] == kExpNaN;
-    e[b] = qe[b] + ke;
-    emin = min(emin, e[b]);
-    emax = max(emax, e[b]);
-  }
-  if (nan) return __uint_as_float(0x7FC00000u);
-  if (emax - emin <= 10 && emin >= -100) {
-    int sum = 0;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) sum += I[b] << (e[b] - emin);
-    return ldexpf((float)sum, emin);
-  }
-  double acc = 0.0;
-#pragma unroll
-  for (int b = 0; b < NB; ++b) acc += (double)I[b] * pow2d(e[b]);
-  return (float)acc;
 }
 
 // true_ex: a = c * 2^e + z per element (c the power-of-two code, 0 for a zero MX
@@ -399,7 +362,10 @@ __device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t,
           sink(j, v, key, std::true_type{});
         }
       };
-#pragma unroll 1
+#ifndef MXA_SEL_KUNROLL
+#define MXA_SEL_KUNROLL 1  // (tools-only builds of other unroll factors for same-box A/Bs)
+#endif
+#pragma unroll MXA_SEL_KUNROLL
       for (int i = 0; i < nt - 1; ++i) one(i, std::false_type{});
       one(nt - 1, std::true_type{});
       if (__builtin_amdgcn_ballot_w64(redo != 0u) != 0) {  // rare: the exact path for those keys
@@ -554,7 +520,7 @@ __device__ __forceinline__ bool sel_rows4(const Rows2Args& a, const SelTabs& t, 
       rec[0] = hand.state | kTailPending;
       kept_put(a, grow * k, 0);
     }
-    for (int p = gl; p < TW; p += 16) rec[4 + p] = (uint32_t)g.A[p];
+    for (int p = gl; p < TW; p += 16) rec[4 + p] = (uint32_t)g.A[p];  // (the tail reads [0, tail_rec_len))
     valid = false;
   } else if (TW > 0 && r < r_end) {  // finished here, or left for the 64-bit pass: not the tail's
     if (gl == 0) a.tail_rec[grow * tail_rec_words(TW)] = 0u;
@@ -600,7 +566,7 @@ __device__ __forceinline__ bool select_item(const Rows2Args& a, unsigned char* s
 // flags, taking the flagged items one after another (a call without such rows costs a
 // small grid that exits at once).
 template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
-__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? kSelPOcc : NP <= 256 ? kSelOcc : 2, 8))) void select_kernel(Rows2Args a) {
+__global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? (TW > 0 ? kSelPOcc : kSelPOccNT) : NP <= 256 ? kSelOcc : 2, 8))) void select_kernel(Rows2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (sizeof(El) == 8 && a.fb_only) {
     __shared__ uint64_t sbits;

@@ -273,37 +273,79 @@ struct TailArgs {
   void* out_vals;
 };
 
+// The introsort stack of a lane, in registers: 16-bit entries (cut | depth << 8), the top in
+// the low bits of s0.  A pushed segment [cut, l) always ends where the entry below it starts
+// (or at m for the bottom entry), so its end is not stored (the pop reads it from the next
+// entry).  At most 2 lg(32) = 10 entries are live (one push per partition step, each costing a
+// level of the depth limit), 12 fit.
+struct TStack {
+  uint64_t s0, s1, s2;
+  __device__ void push(uint32_t e) {
+    s2 = (s2 << 16) | (s1 >> 48);
+    s1 = (s1 << 16) | (s0 >> 48);
+    s0 = (s0 << 16) | e;
+  }
+  __device__ uint32_t pop() {
+    const uint32_t e = (uint32_t)s0 & 0xFFFFu;
+    s0 = (s0 >> 16) | (s1 << 48);
+    s1 = (s1 >> 16) | (s2 << 48);
+    s2 >>= 16;
+    return e;
+  }
+  __device__ uint32_t top() const { return (uint32_t)s0 & 0xFFFFu; }
+};
+
 // one lane per row; a workgroup of kTailWaves waves, each wave's 64 rows' prefixes in LDS
+// (TW words per lane: the introsort stack lives in registers, the prune-mask words are set
+// in the prefix's positions [k, k + ntw) once the kept elements are in registers)
 constexpr int kTailWaves = 1;
-constexpr int kTailStk = 12;  // introsort stack entries (depth limit 2 lg(32) + 1 = 11)
 constexpr int kTailMaxK = 33;  // k handed to the tail (k - 1 <= 32: the final rank's width)
+// the record's positions the tail reads: [0, l) of an introselect hand-over (nothing past the
+// range is read again: the window loads beyond l are masked out of the stop masks), [0, k - 1)
+// of a sort hand-over
+__device__ __forceinline__ int tail_rec_len(uint32_t state, int k) {
+  return ((state >> 24) & 3u) ? k - 1 : (int)((state >> 8) & 0xFFu);
+}
 template <int TW>
 __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (64 * kTailWaves) + threadIdx.x;
-  const TPtr A{(tl32*)(lu32*)(smem) + (size_t)wave * 64 * (TW + kTailStk) + lane};
-  const TPtr stk = A + TW;  // introsort stack: kTailStk entries after the prefix
+  const TPtr A{(tl32*)(lu32*)(smem) + (size_t)wave * 64 * TW + lane};
+  const int k = a.k, nth = k - 1, m = k - 1;
   uint32_t st = 0u;
   if (row < a.rows) {
     const uint32_t* src = a.rec + row * tail_rec_words(TW);
     st = src[0];
-    if (st & kTailPending) {
+    if (st & kTailPending) {  // all loads first, then the LDS stores (one wait)
+      const int len = tail_rec_len(st, k);
+      uint4 v[TW / 4];
+#pragma unroll
+      for (int e = 0; e < TW; e += 4)
+        v[e / 4] = e < len ? *reinterpret_cast<const uint4*>(src + 4 + e) : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int e = 0; e < TW; e += 4) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + 4 + e);
-        A[e] = v.x;
-        A[e + 1] = v.y;
-        A[e + 2] = v.z;
-        A[e + 3] = v.w;
+        A[e] = v[e / 4].x;
+        A[e + 1] = v[e / 4].y;
+        A[e + 2] = v[e / 4].z;
+        A[e + 3] = v[e / 4].w;
       }
     }
   }
   const bool pend = (st & kTailPending) != 0;
-  const int k = a.k, nth = k - 1, m = k - 1;
+#ifdef MXA_TAIL_SKIP  // tools-only phase timing (build_native defines): 4 = the record loads alone
+  if ((MXA_TAIL_SKIP) & 4) {
+    if (pend && row < a.rows) {
+      if (a.idx_out) a.idx_out[row * k] = (int64_t)((uint32_t)A[0] & 0xFFu);
+      else a.idx16[row * k] = (uint16_t)((uint32_t)A[0] & 0xFFu);
+    }
+    return;
+  }
+#endif
   int f = (int)(st & 0xFFu), l = (int)((st >> 8) & 0xFFu), d = (int)((st >> 16) & 0xFFu);
   int ph = pend ? (int)((st >> 24) & 0x3u) : 2;  // 0 introselect, 1 introsort loop, 2 done
   int sp = 0;
+  TStack stk{0, 0, 0};
   if (ph == 1) {
     f = 0;
     l = m;
@@ -311,6 +353,12 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
   }
   while (true) {
     if (ph == 0 && (l - f <= 3 || d == 0)) {  // the selection ends
+#ifdef MXA_TAIL_SKIP  // 2 = no sort of [0, k-1) (and no rank)
+      if ((MXA_TAIL_SKIP) & 2) {
+        ph = 2;
+        continue;
+      }
+#endif
       if (l - f > 3) {  // depth limit: __heap_select(f, nth + 1, l); iter_swap(f, nth)
         tn_heap_select(A, f, nth + 1, l);
         const uint32_t tt = A[f];
@@ -335,10 +383,10 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
           break;
         }
         --sp;
-        const uint32_t e = stk[sp];
+        const uint32_t e = stk.pop();
         f = (int)(e & 0xFFu);
-        l = (int)((e >> 8) & 0xFFu);
-        d = (int)(e >> 16);
+        d = (int)(e >> 8);
+        l = sp > 0 ? (int)(stk.top() & 0xFFu) : m;  // the segment ends where the next one starts
       }
     }
     const bool act = ph < 2;
@@ -350,13 +398,16 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
         if (cut <= nth) f = cut;
         else l = cut;
       } else {
-        stk[sp] = (uint32_t)cut | ((uint32_t)l << 8) | ((uint32_t)d << 16);  // __introsort_loop(cut, l)
+        stk.push((uint32_t)cut | ((uint32_t)d << 8));  // __introsort_loop(cut, l)
         ++sp;
         l = cut;
       }
     }
   }
   // std::sort's final insertion sort = a stable rank of [0, m) (segments mutually ordered)
+#ifdef MXA_TAIL_SKIP  // 1 = no final rank
+  if ((MXA_TAIL_SKIP) & 1) ph = 2;
+#endif
   if (__builtin_amdgcn_ballot_w64(ph == 3 && m >= 2) != 0) {  // (m <= 32: sel_tail_width)
     if (m <= 16) {
       if (ph == 3) t_rank<16>(A, m);
@@ -369,28 +420,32 @@ __global__ __launch_bounds__(64 * kTailWaves) void topk_tail_kernel(TailArgs a) 
     }
   }
   if (!pend) return;
-  // the kept indices (k <= kTailMaxK: sel_tail_width / topk_ws_tw), and the prune-mask words
-  // (zeros.scatter_(-1, idx, 1) as bits) set in the lane's own stack slots (free now; ntw <= 8
-  // < kTailStk) by LDS ORs; the standalone top-k's values at the kept indices come back from
-  // the packed elements themselves (q_value: no gather from the input rows)
-  uint32_t ix[kTailMaxK];
+  // the kept elements (k <= kTailMaxK: sel_tail_width / topk_ws_tw) into registers, then the
+  // prune-mask words (zeros.scatter_(-1, idx, 1) as bits) set by LDS ORs in the prefix's free
+  // positions [k, k + ntw) (k + ntw <= TW: sel_tail_width); the standalone top-k's values at the
+  // kept indices come back from the packed elements themselves (q_value: no gather from the
+  // input rows)
+  uint32_t x[kTailMaxK];
 #pragma unroll
-  for (int p = 0; p < kTailMaxK; ++p) ix[p] = p < k ? (uint32_t)A[p] & 0xFFu : 0u;
+  for (int p = 0; p < kTailMaxK; ++p) x[p] = p < k ? (uint32_t)A[p] : 0u;
   const int ntw = a.mask_out ? a.ntw : 0;
-  for (int w = 0; w < ntw; ++w) stk[w] = 0u;
+  for (int w = 0; w < ntw; ++w) A[k + w] = 0u;
 #pragma unroll
   for (int p = 0; p < kTailMaxK; ++p) {
     if (p < k) {
-      if (a.idx_out) a.idx_out[row * k + p] = (int64_t)ix[p];
-      else a.idx16[row * k + p] = (uint16_t)ix[p];
-      if (ntw) __hip_atomic_fetch_or(stk[(int)(ix[p] >> 5)].p, 1u << (ix[p] & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint32_t ix = x[p] & 0xFFu;
+      if (a.idx_out) a.idx_out[row * k + p] = (int64_t)ix;
+      else a.idx16[row * k + p] = (uint16_t)ix;
+      if (ntw) __hip_atomic_fetch_or(A[k + (int)(ix >> 5)].p, 1u << (ix & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
-  for (int w = 0; w < ntw; ++w) a.mask_out[row * ntw + w] = (uint32_t)stk[w];
+  for (int w = 0; w < ntw; ++w) a.mask_out[row * ntw + w] = (uint32_t)A[k + w];
   if (a.out_vals)  // (the packed pass sent no row with a NaN or -0 value: q_val_bad)
-    for (int p = 0; p < k; ++p) store_dt(a.out_vals, row * k + p, q_value((uint32_t)A[p]), a.dt);
+#pragma unroll
+    for (int p = 0; p < kTailMaxK; ++p)
+      if (p < k) store_dt(a.out_vals, row * k + p, q_value(x[p]), a.dt);
 }
 
-__host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * (TW + kTailStk) * 4; }
+__host__ __device__ constexpr size_t tail_lds(int TW) { return (size_t)kTailWaves * 64 * TW * 4; }
 
 }  // namespace mxa
