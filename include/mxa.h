@@ -347,6 +347,13 @@ int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, 
                int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype,
                int32_t b_dtype, int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream);
 int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t K, int32_t Nc);
+/* mxa_matmul with in2 given transposed: bt (batch, Nc, K) row-major, i.e. in2 = bt^T (the
+ * k.transpose(-2, -1) view of deit main.py:101, DiT models.py:169), quantized along K as in
+ * mxa_matmul -- no copy of the transposed operand.  Same workspace (mxa_matmul_workspace_bytes). */
+int mxa_matmul_bt(const void* a, const void* bt, void* c, int64_t batch, int32_t M, int32_t K,
+                  int32_t Nc, int64_t a_batch_stride, int64_t bt_batch_stride, int32_t elem_mbits_a,
+                  int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype,
+                  int32_t b_dtype, int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream);
 
 /* Self-tests of the int8 MFMA operand/accumulator lane maps the kernels rely on:
  * C = A * B computed by one MFMA, row-major int8 operands, int32 result; the host

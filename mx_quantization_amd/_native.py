@@ -102,6 +102,8 @@ _SIGS = {
     "mxa_matmul": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
                            c_i32, c_i32, c_i32, c_vp, c_i64, c_vp]),
     "mxa_matmul_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i32]),
+    "mxa_matmul_bt": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, c_i32,
+                              c_i32, c_i32, c_i32, c_vp, c_i64, c_vp]),
     "mxa_selftest_mfma": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
     "mxa_selftest_mfma32": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
 }

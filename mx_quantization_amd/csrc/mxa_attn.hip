@@ -75,7 +75,7 @@ struct AttnLayout {
   int nbd, dpad, ntb, tpad;
   int64_t qc, qop, qz, qsT, qsA, qsg, kc, kop, kz, ksT, ksA, ksg, knorm, vt, vs, idx16, tail, fbf, mask;
   int64_t xc, xs;  // fused qkv projection: x codes / exponents
-  int64_t yc, ys, yf, yslow;  // fused proj Linear: its input codes / exponents, the fp32 output
+  int64_t yc, ys, yf;  // fused proj Linear: its input codes / exponents, the fp32 output
                               // copy (D % 32 != 0 only), the GEMM's fp64 wave list
   int64_t total;
 };
@@ -154,7 +154,6 @@ AttnLayout attn_layout(const mxa_attn_params* p, int mode, const mxa_qkv_params*
     L.yc = take((tokens + 31) / 32 * 32 * nbk * 32);  // MFMA-ready codes: whole 32-row blocks
     L.ys = take(tokens * nbk * 2);
     L.yf = take(proj_codes_direct(p) ? 0 : tokens * C * 4);
-    L.yslow = take(gemm_slow_bytes((int)std::min<int64_t>(tokens, INT32_MAX), pj->out_features, 1));
   }
   L.total = off;
   return L;
@@ -438,7 +437,7 @@ static int attention_impl(const mxa_attn_params* p, hipStream_t stream, hipEvent
       if (rc) return rc;
     }
     rc = launch_linear_codes(yc, ys, tokens, C, pj->wq, pj->out_features, pj->bias, pj->y, pj->y_row_stride,
-                             pp.bfloat, 0, reinterpret_cast<int*>(ws + L.yslow), stream, true);
+                             pp.bfloat, 0, stream, true);
     if (rc) return rc;
     if (ev) (void)hipEventRecord(ev[6], stream);
   }
@@ -537,13 +536,17 @@ extern "C" int64_t mxa_matmul_workspace_bytes(int64_t batch, int32_t M, int32_t 
   if (batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return -1;
   const int64_t nbk = (K + 31) / 32, kpad = nbk * 32;
   return align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) + align_up(batch * Nc * kpad) +
-         align_up(batch * nbk * Nc * 2) + gemm_slow_bytes(M, Nc, std::min<int64_t>(batch, 65535));
+         align_up(batch * nbk * Nc * 2);
 }
 
-extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
-                          int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a, int32_t elem_mbits_b,
-                          int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype, int32_t b_dtype,
-                          int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+// in2 given as b (batch, K, Nc) row-major (cols_prep: codes transposed to [Nc][kpad],
+// exponents [nbk][Nc]) or, bt_rows, as its transpose bt (batch, Nc, K) row-major (rows_prep:
+// the same codes and blocks along K, exponents [Nc][nbk]) -- the k.transpose(-2, -1) view of
+// the callers needs no copy
+static int matmul_impl(const void* a, const void* b, bool bt_rows, void* c, int64_t batch, int32_t M, int32_t K,
+                       int32_t Nc, int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a,
+                       int32_t elem_mbits_b, int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype, int32_t b_dtype,
+                       int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
   if (!a || !b || !c || batch <= 0 || M <= 0 || K <= 0 || Nc <= 0) return MXA_ERR_ARG;
   for (int dt : {a_dtype, b_dtype, c_dtype})
     if (dt < MXA_DT_F32 || dt > MXA_DT_BF16) return MXA_ERR_ARG;
@@ -559,34 +562,57 @@ extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, 
   int8_t* bt = reinterpret_cast<int8_t*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2));
   int16_t* bsc = reinterpret_cast<int16_t*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) +
                                             align_up(batch * Nc * kpad));
-  RowsPrepArgs ra{};
-  ra.x = a; ra.s0 = a_batch_stride; ra.s1 = 0; ra.s2 = K; ra.H = 1; ra.R = M; ra.rows = batch * M;
-  ra.D = K; ra.nb = nbk; ra.dpad = kpad;
-  const int64_t vpe = a_dtype == MXA_DT_F32 ? 4 : 8;
-  ra.vec4 = aligned16(a) && (a_batch_stride % vpe == 0) && (K % vpe == 0);
-  ra.op_kind = elem_mbits_a == 8 ? MXA_OP_MXINT8 : MXA_OP_MXINT4;
-  ra.flush = flush_subnormals; ra.bfloat = bfloat; ra.dt = a_dtype;
-  ra.codes = nullptr; ra.sT = nullptr; ra.op = ac; ra.sA = as;
-  int rc = launch_rows_prep(ra, stream);
+  // MX rows along K (rows_prep): a, and b's transpose when given so
+  auto rows_mx = [&](const void* x, int64_t bstride, int R, int mbits, int dt, int8_t* codes, int16_t* exps) {
+    RowsPrepArgs ra{};
+    ra.x = x; ra.s0 = bstride; ra.s1 = 0; ra.s2 = K; ra.H = 1; ra.R = R; ra.rows = batch * R;
+    ra.D = K; ra.nb = nbk; ra.dpad = kpad;
+    const int64_t vpe = dt == MXA_DT_F32 ? 4 : 8;
+    ra.vec4 = aligned16(x) && (bstride % vpe == 0) && (K % vpe == 0);
+    ra.op_kind = mbits == 8 ? MXA_OP_MXINT8 : MXA_OP_MXINT4;
+    ra.flush = flush_subnormals; ra.bfloat = bfloat; ra.dt = dt;
+    ra.codes = nullptr; ra.sT = nullptr; ra.op = codes; ra.sA = exps;
+    return launch_rows_prep(ra, stream);
+  };
+  int rc = rows_mx(a, a_batch_stride, M, elem_mbits_a, a_dtype, ac, as);
   if (rc) return rc;
-  ColsPrepArgs cb{};
-  cb.x = b; cb.s0 = b_batch_stride; cb.s1 = 0; cb.s2 = Nc; cb.H = 1; cb.mats = batch; cb.R = K; cb.C = Nc;
-  cb.nb = nbk; cb.rpad = kpad; cb.mbits = elem_mbits_b; cb.flush = flush_subnormals; cb.bfloat = bfloat; cb.dt = b_dtype;
-  cb.codes_t = bt; cb.scale = bsc;
-  rc = launch_cols_prep(cb, stream);
+  if (bt_rows) {
+    rc = rows_mx(b, b_batch_stride, Nc, elem_mbits_b, b_dtype, bt, bsc);
+  } else {
+    ColsPrepArgs cb{};
+    cb.x = b; cb.s0 = b_batch_stride; cb.s1 = 0; cb.s2 = Nc; cb.H = 1; cb.mats = batch; cb.R = K; cb.C = Nc;
+    cb.nb = nbk; cb.rpad = kpad; cb.mbits = elem_mbits_b; cb.flush = flush_subnormals; cb.bfloat = bfloat; cb.dt = b_dtype;
+    cb.codes_t = bt; cb.scale = bsc;
+    rc = launch_cols_prep(cb, stream);
+  }
   if (rc) return rc;
   // C[b] = MX(A[b]) @ MX(B[b]) on the block-scaled GEMM (mxa_gemm.hpp): A's MX codes
-  // row-major along K, B's transposed codes [Nc][kpad], exponents [nbk][Nc]
+  // row-major along K, B's transposed codes [Nc][kpad], exponents [nbk][Nc] or [Nc][nbk]
   GemmArgs g{};
   g.a = ac; g.ae = as; g.a_bat = (int64_t)M * kpad; g.ae_bat = (int64_t)M * nbk; g.lda = kpad;
   g.b = bt; g.b_bat = (int64_t)Nc * kpad; g.ldb = kpad;
-  g.be = bsc; g.be_bat = (int64_t)nbk * Nc; g.be_n = 1; g.be_k = Nc;
+  g.be = bsc; g.be_bat = (int64_t)nbk * Nc;
+  g.be_n = bt_rows ? nbk : 1; g.be_k = bt_rows ? 1 : Nc;
   g.M = M; g.Nc = Nc; g.nbk = nbk;
   g.linear = 0; g.dt = c_dtype; g.bfloat = bfloat;
   g.c = c; g.c_bat = (int64_t)M * Nc; g.ldc = Nc;
-  int* slow = reinterpret_cast<int*>(ws + align_up(batch * M * kpad) + align_up(batch * M * nbk * 2) +
-                                     align_up(batch * Nc * kpad) + align_up(batch * nbk * Nc * 2));
-  return launch_gemm(g, batch, slow, stream);
+  return launch_gemm(g, batch, stream);
+}
+
+extern "C" int mxa_matmul(const void* a, const void* b, void* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
+                          int64_t a_batch_stride, int64_t b_batch_stride, int32_t elem_mbits_a, int32_t elem_mbits_b,
+                          int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype, int32_t b_dtype,
+                          int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  return matmul_impl(a, b, false, c, batch, M, K, Nc, a_batch_stride, b_batch_stride, elem_mbits_a, elem_mbits_b,
+                     flush_subnormals, bfloat, a_dtype, b_dtype, c_dtype, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mxa_matmul_bt(const void* a, const void* bt, void* c, int64_t batch, int32_t M, int32_t K, int32_t Nc,
+                             int64_t a_batch_stride, int64_t bt_batch_stride, int32_t elem_mbits_a, int32_t elem_mbits_b,
+                             int32_t flush_subnormals, int32_t bfloat, int32_t a_dtype, int32_t b_dtype,
+                             int32_t c_dtype, void* workspace, int64_t workspace_bytes, hipStream_t stream) {
+  return matmul_impl(a, bt, true, c, batch, M, K, Nc, a_batch_stride, bt_batch_stride, elem_mbits_a, elem_mbits_b,
+                     flush_subnormals, bfloat, a_dtype, b_dtype, c_dtype, workspace, workspace_bytes, stream);
 }
 
 extern "C" int mxa_selftest_mfma32(const int8_t* a, const int8_t* b, int32_t* c, hipStream_t stream) {

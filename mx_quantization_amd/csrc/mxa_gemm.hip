@@ -14,24 +14,13 @@ int gemm_smax(int nbk) {
   return s;
 }
 
-// the fp64 kernel's list (count, then tile * 4 + wave entries)
-static int64_t gemm_tiles(int M, int Nc, int64_t batch) {
-  return (int64_t)((M + kGemmRows - 1) / kGemmRows) * ((Nc + kGemmCols - 1) / kGemmCols) * batch;
-}
-int64_t gemm_slow_bytes(int M, int Nc, int64_t batch) { return (4 * (2 + 4 * gemm_tiles(M, Nc, batch)) + 255) / 256 * 256; }
-
-// slow: gemm_slow_bytes of device scratch (the fp64 kernel's list)
 template <bool PLAIN>
-static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, int* slow, hipStream_t stream) {
+static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, hipStream_t stream) {
   GemmArgs ga = ga0;
   ga.smax = gemm_smax(ga.nbk);
   const size_t lds = gemm_lds(ga.nbk).total;
   const int64_t gx = (ga.Nc + kGemmCols - 1) / kGemmCols, gy = (ga.M + kGemmRows - 1) / kGemmRows;
-  if (lds > 160 * 1024 || gy > 65535 || gx * gy * batch * 4 >= ((int64_t)1 << 31)) return MXA_ERR_UNSUPPORTED;
-  for (const void* k : {reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN>),
-                        reinterpret_cast<const void*>(&mx_gemm_slow_kernel<PLAIN>)})
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
-  ga.slow = slow;
+  if (lds > 160 * 1024 || gy > 65535) return MXA_ERR_UNSUPPORTED;
   if (ga.bpd && batch == 1 && ga.nbk <= kGemmDigNbkMax) {
     // a prepared weight: the exponent-folded digits, every row block in the one launch (a
     // block the digits cannot take sums its K-blocks in fp64 in the same workgroup)
@@ -41,34 +30,33 @@ static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, int* slow, hipStrea
     hipLaunchKernelGGL(mx_gemm_dig_kernel<PLAIN>, dim3((unsigned)((ga.M + 31) / 32)), dim3(256), dl, stream, ga);
     return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
   }
-  // grid.z <= 65535: larger batches in slices (each slice lists its slow waves by its own
-  // batch index, so every slice runs its own fp64 pass)
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return MXA_ERR_LAUNCH;
+  // grid.z <= 65535: larger batches in slices; a wave whose spreads the int32 sums cannot
+  // take sums its blocks in fp64 itself (gemm_tile's run_f64): one launch per slice
   const int64_t esz = (ga.linear || ga.dt == kF32) ? 4 : 2;
   for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
     GemmArgs gs = ga;
     gs.a += b0 * ga.a_bat; gs.ae += b0 * ga.ae_bat; gs.b += b0 * ga.b_bat; gs.be += b0 * ga.be_bat;
     gs.c = static_cast<unsigned char*>(ga.c) + b0 * ga.c_bat * esz;
     const int64_t nb = std::min<int64_t>(65535, batch - b0);
-    if (hipMemsetAsync(slow, 0, sizeof(int), stream) != hipSuccess) return MXA_ERR_LAUNCH;
     hipLaunchKernelGGL(mx_gemm_kernel<PLAIN>, dim3((unsigned)gx, (unsigned)gy, (unsigned)nb), dim3(256), lds, stream, gs);
-    if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
-    const unsigned sgrid = (unsigned)std::min<int64_t>(gx * gy * nb * 4, 1024);
-    hipLaunchKernelGGL(mx_gemm_slow_kernel<PLAIN>, dim3(sgrid), dim3(256), lds, stream, gs);
     if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   }
   return MXA_OK;
 }
 
-int launch_gemm(const GemmArgs& ga, int64_t batch, int* slow, hipStream_t stream) {
-  if (ga.M <= 0 || ga.Nc <= 0 || ga.nbk <= 0 || batch <= 0 || !slow) return MXA_ERR_ARG;
+int launch_gemm(const GemmArgs& ga, int64_t batch, hipStream_t stream) {
+  if (ga.M <= 0 || ga.Nc <= 0 || ga.nbk <= 0 || batch <= 0) return MXA_ERR_ARG;
   const bool plain = (ga.bfloat == 0 || ga.bfloat == 32) && (ga.linear ? ga.autocast == 0 : ga.dt == kF32);
-  return plain ? launch_gemm_p<true>(ga, batch, slow, stream) : launch_gemm_p<false>(ga, batch, slow, stream);
+  return plain ? launch_gemm_p<true>(ga, batch, stream) : launch_gemm_p<false>(ga, batch, stream);
 }
 
 // GEMM of MX rows (rows_prep layout: codes [rows][Cpad], exponents [rows][nbk]) with a
 // prepared Linear weight (its row-major codes / exponents): out = mx.Linear epilogue
 int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int in_f, const void* wq, int out_f,
-                        const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast, int* slow,
+                        const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast,
                         hipStream_t stream, bool x_mfma) {
   const LinearLayout W = linear_layout(out_f, in_f, out_f);  // raw regions do not depend on gw
   const unsigned char* wb = static_cast<const unsigned char*>(wq);
@@ -93,7 +81,7 @@ int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int i
   g.linear = 1; g.dt = kF32; g.bfloat = bfloat; g.autocast = autocast; g.bias = bias;
   g.c = out; g.ldc = out_row_stride;
   if (rows > ((int64_t)1 << 31) - 1) return MXA_ERR_UNSUPPORTED;
-  return launch_gemm(g, 1, slow, stream);
+  return launch_gemm(g, 1, stream);
 }
 
 }  // namespace mxa
@@ -104,8 +92,7 @@ extern "C" int64_t mxa_linear_workspace_bytes(int64_t rows, int32_t in_features,
   if (rows <= 0 || in_features <= 0 || out_features <= 0 || rows > INT32_MAX) return -1;
   const int64_t nbk = (in_features + 31) / 32;
   const int64_t rows32 = (rows + 31) / 32 * 32;  // the MFMA-ready codes hold whole 32-row blocks
-  return (rows32 * nbk * 32 + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256 +
-         gemm_slow_bytes((int)rows, out_features, 1);
+  return (rows32 * nbk * 32 + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256;
 }
 
 extern "C" int mxa_linear(const float* x, int64_t rows, int32_t in_features, int64_t x_row_stride, const void* wq,
@@ -134,7 +121,6 @@ extern "C" int mxa_linear(const float* x, int64_t rows, int32_t in_features, int
   rx.sT = reinterpret_cast<int16_t*>(ws + (rows32 * Cpad + 255) / 256 * 256);
   int rc = launch_rows_prep(rx, stream);
   if (rc) return rc;
-  int* slow = reinterpret_cast<int*>(ws + (rows32 * Cpad + 255) / 256 * 256 + (rows * nbk * 2 + 255) / 256 * 256);
   return launch_linear_codes(rx.codes, rx.sT, rows, in_features, wq, out_features, bias, out, out_row_stride, bfloat,
-                             autocast_dtype, slow, stream, true);
+                             autocast_dtype, stream, true);
 }

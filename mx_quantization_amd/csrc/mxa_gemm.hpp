@@ -59,14 +59,12 @@ __host__ __device__ inline GemmLds gemm_lds(int nbk) {
   return L;
 }
 
-// SLOW = false: the shifted-int32 path; a wave that fails its test appends its tile to
-// a.slow (count, then entries) and leaves.  SLOW = true: a fixed grid strides over that
-// list and sums those waves' blocks in fp64 (an empty list costs one read per workgroup).
+// The shifted-int32 path; a wave whose spreads fail its test sums its blocks in fp64 itself
+// (run_f64: no list, no follow-up kernel).
 // PLAIN: float32 output, no bfloat / autocast rounding (the bench and workload settings):
 // the epilogue is a store (+ bias), compiled without the general rounding code.
-template <bool SLOW, bool PLAIN>
-__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm, int tn, int only_wave,
-                                          unsigned char* smem) {
+template <bool PLAIN>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm, int tn, unsigned char* smem) {
   typedef int v16i_g __attribute__((ext_vector_type(16)));
   typedef int v4i_g __attribute__((ext_vector_type(4)));
   const int nbk = a.nbk;
@@ -201,17 +199,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   const int srow = wmax(rv ? rsp : 0), scol = wmax(cv ? csp : 0);
   const int lrow = wmin(rv ? rlo[rr] : (1 << 19)), lcol = wmin(cv ? clo[cc] : (1 << 19));
   const bool fast = srow + scol <= a.smax && lrow + lcol >= -126;
-  if constexpr (!SLOW) {
-    if (!fast) {
-      if (lane == 0) {
-        const int64_t ntm = (a.M + kGemmRows - 1) / kGemmRows, ntn = (a.Nc + kGemmCols - 1) / kGemmCols;
-        a.slow[1 + atomicAdd(a.slow, 1)] = (int)(((bat * ntm + tm) * ntn + tn) * 4 + wave);
-      }
-      return;
-    }
-  } else {
-    if (wave != only_wave) return;
-  }
 
   const int arow = min(m0g + wr0 + ln, a.M - 1);
   const int bc0 = min(n0g + wc0 + ln, a.Nc - 1), bc1 = min(n0g + wc0 + 32 + ln, a.Nc - 1);
@@ -264,7 +251,31 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     }
   };
 
-  if constexpr (!SLOW) {
+  // fp64 block sums, one chain at a time (registers for one double accumulator set): the
+  // waves whose spreads could overflow int32 (or whose result could be subnormal)
+  auto run_f64 = [&]() {
+    for (int j = 0; j < 2; ++j) {
+      const int8_t* bp = j ? bp1 : bp0;
+      const int lc = clo[wc0 + 32 * j + ln];
+      double acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+      for (int kb = 0; kb < nbk; ++kb) {
+        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ldb(bp, kb), zero, 0, 0, 0);
+        const int dc = xcol[kb * kGemmCols + 32 * j] + lc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3);
+          acc[i] += ldexp((double)c[i], xe[kb * kGemmRows + lr] + rlo[lr] + dc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) store(j, i, (float)acc[i]);
+    }
+  };
+  if (!fast) {
+    run_f64();
+  } else {
     int acc0[16], acc1[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0;
@@ -315,26 +326,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
       store(0, i, ldexpf((float)acc0[i], lr + lc0));
       store(1, i, ldexpf((float)acc1[i], lr + lc1));
     }
-  } else {
-    // fp64 block sums, one chain at a time (registers for one double accumulator set)
-    for (int j = 0; j < 2; ++j) {
-      const int8_t* bp = j ? bp1 : bp0;
-      const int lc = clo[wc0 + 32 * j + ln];
-      double acc[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-      for (int kb = 0; kb < nbk; ++kb) {
-        const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ldb(bp, kb), zero, 0, 0, 0);
-        const int dc = xcol[kb * kGemmCols + 32 * j] + lc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3);
-          acc[i] += ldexp((double)c[i], xe[kb * kGemmRows + lr] + rlo[lr] + dc);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) store(j, i, (float)acc[i]);
-    }
   }
 }
 
@@ -342,22 +333,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
 template <bool PLAIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void mx_gemm_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemm_tile<false, PLAIN>(a, blockIdx.z, blockIdx.y, blockIdx.x, -1, smem);
-}
-
-template <bool PLAIN>
-__global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int n = __builtin_amdgcn_readfirstlane(*a.slow);
-  const int64_t ntm = (a.M + kGemmRows - 1) / kGemmRows, ntn = (a.Nc + kGemmCols - 1) / kGemmCols;
-  for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    const int64_t e = __builtin_amdgcn_readfirstlane(a.slow[1 + i]);
-    const int w = (int)(e & 3);
-    const int64_t t = e >> 2;
-    const int tn = (int)(t % ntn), tm = (int)((t / ntn) % ntm);
-    gemm_tile<true, PLAIN>(a, t / (ntn * ntm), tm, tn, w, smem);
-    __syncthreads();  // the next entry restages the exponent tables
-  }
+  gemm_tile<PLAIN>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
 }
 
 // ---- exponent-folded digits (mx.Linear with a prepared weight) ----------------------
@@ -370,7 +346,7 @@ __global__ __launch_bounds__(256) void mx_gemm_slow_kernel(GemmArgs a) {
 // rounded exact product as gemm_tile's shifted int32 sums.  A row block whose spreads or
 // the weight's column spreads exceed kDigitSpread (or whose result could be subnormal) is
 // summed here block by block in fp64 instead (the MFMA-ready weight codes, ascending
-// K-blocks: the sums of mx_gemm_slow_kernel, exact while the scaled blocks span <= 34 bits
+// K-blocks: the sums of gemm_tile's run_f64, exact while the scaled blocks span <= 34 bits
 // -- so also wherever the shifted int32 sums are exact), so one launch covers every row
 // block: no flag, no follow-up kernels.
 struct GemmDigLds {

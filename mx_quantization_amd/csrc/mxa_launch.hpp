@@ -99,10 +99,9 @@ bool linear_weight_verify_any_group(const void* wq, int out_f, int in_f, int flu
 bool linear_weight_known_header(const void* wq, LinearWeightHeader* h);
 // block-scaled MX GEMM (mxa_gemm.hip); mx.Linear on MX rows with a prepared weight
 // (slow: gemm_slow_bytes of device scratch for the list of waves the fp64 kernel takes)
-int64_t gemm_slow_bytes(int M, int Nc, int64_t batch);
-int launch_gemm(const GemmArgs& ga, int64_t batch, int* slow, hipStream_t stream);
+int launch_gemm(const GemmArgs& ga, int64_t batch, hipStream_t stream);
 int launch_linear_codes(const int8_t* xc, const int16_t* xs, int64_t rows, int in_f, const void* wq, int out_f,
-                        const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast, int* slow,
+                        const float* bias, float* out, int64_t out_row_stride, int bfloat, int autocast,
                         hipStream_t stream, bool x_mfma);
 
 }  // namespace mxa

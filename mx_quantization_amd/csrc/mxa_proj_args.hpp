@@ -122,7 +122,6 @@ struct GemmArgs {
   const float* bias;  // linear: [Nc] or null
   void* c;            // (bat, m, n) at bat * c_bat + m * ldc + n
   int64_t c_bat, ldc;
-  int* slow;  // waves for the fp64 kernel: count, then (tile * 4 + wave); zeroed before the launch
   // optional MFMA-ready B (a prepared Linear weight's pk, one group: columns in 32-column
   // blocks, [cb][kb][lane][16 B]): one coalesced 1-KB load per wave, chain and K-block
   const int8_t* bpk;

@@ -186,7 +186,13 @@ def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbit
     if K != K2:
         raise ValueError(f"inner dimensions differ: {K} vs {K2}")
     a = a.expand(batch_shape + (M, K)).contiguous()
-    b = b.expand(batch_shape + (K, Nc)).contiguous()
+    b = b.expand(batch_shape + (K, Nc))
+    # b the transpose of a row-major (..., Nc, K) tensor (the callers' k.transpose(-2, -1)):
+    # quantized from that layout along K (mxa_matmul_bt), no copy
+    bt = b.transpose(-2, -1)
+    transposed = bt.is_contiguous()
+    if not transposed:
+        b = b.contiguous()
     batch = 1
     for s in batch_shape:
         batch *= s
@@ -197,9 +203,9 @@ def mx_matmul(a: torch.Tensor, b: torch.Tensor, elem_mbits_a: int = 8, elem_mbit
         return c.zero_()
     nbytes = lib().mxa_matmul_workspace_bytes(batch, M, K, Nc)
     ws = _workspace(dev, nbytes)
-    check(lib().mxa_matmul(a.data_ptr(), b.data_ptr(), c.data_ptr(), batch, M, K, Nc, M * K, K * Nc, elem_mbits_a,
-                           elem_mbits_b, int(flush), int(bfloat), adt, bdt, cdt, ws.data_ptr(), ws.numel(),
-                           stream_ptr(dev)), "mxa_matmul")
+    fn, bp = (lib().mxa_matmul_bt, bt.data_ptr()) if transposed else (lib().mxa_matmul, b.data_ptr())
+    check(fn(a.data_ptr(), bp, c.data_ptr(), batch, M, K, Nc, M * K, K * Nc, elem_mbits_a, elem_mbits_b, int(flush),
+             int(bfloat), adt, bdt, cdt, ws.data_ptr(), ws.numel(), stream_ptr(dev)), "mxa_matmul")
     return c
 
 

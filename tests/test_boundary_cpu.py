@@ -54,9 +54,9 @@ def test_workspace_formula():
     nbytes = N.lib().mxa_attention_workspace_bytes(ctypes.byref(p))
     # per head: Q,K codes + exponents + sign words (2 x 197 x (64 + 4 + 4 + 8) B),
     # V^T codes + exponents (64 x 224 + 7 x 64 x 2 B), kept indices (197 x 20 x 2 B: the
-    # 16-bit copy for callers without idx), the one-lane tail's records (197 x (64 + 4) x 4 B:
-    # k = 20 takes the 64-position prefix), the packed pass's flags (13 x 4 B: one per 16 rows)
-    per_head = 2 * 197 * (64 + 4 + 4 + 8) + 64 * 224 + 7 * 64 * 2 + 197 * 20 * 2 + 197 * 68 * 4 + 13 * 4
+    # 16-bit copy for callers without idx), the one-lane tail's records (197 x (48 + 4) x 4 B:
+    # k = 20 takes the 48-position prefix), the packed pass's flags (13 x 4 B: one per 16 rows)
+    per_head = 2 * 197 * (64 + 4 + 4 + 8) + 64 * 224 + 7 * 64 * 2 + 197 * 20 * 2 + 197 * 52 * 4 + 13 * 4
     assert 3072 * per_head <= nbytes < 3072 * per_head + 17 * 256
 
 
