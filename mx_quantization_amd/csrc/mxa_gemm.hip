@@ -18,8 +18,15 @@ template <bool PLAIN>
 static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, hipStream_t stream) {
   GemmArgs ga = ga0;
   ga.smax = gemm_smax(ga.nbk);
-  const size_t lds = gemm_lds(ga.nbk).total;
-  const int64_t gx = (ga.Nc + kGemmCols - 1) / kGemmCols, gy = (ga.M + kGemmRows - 1) / kGemmRows;
+  // the tile shape (mxa_gemm.hpp GemmShape): products of <= 64 columns on 128 x 64 tiles;
+  // float32 products of 65..256 contiguous columns on 32-row strips of whole rows; else 64 x 128
+  const int sh = ga.Nc <= GemmShape<kGemmTall>::CW                           ? kGemmTall
+                 : PLAIN && ga.Nc <= GemmShape<kGemmWide>::CW && ga.ldc == ga.Nc ? kGemmWide
+                                                                              : kGemmSquare;
+  const int RW = sh == kGemmTall ? GemmShape<kGemmTall>::RW : sh == kGemmWide ? GemmShape<kGemmWide>::RW : GemmShape<kGemmSquare>::RW;
+  const int CW = sh == kGemmTall ? GemmShape<kGemmTall>::CW : sh == kGemmWide ? GemmShape<kGemmWide>::CW : GemmShape<kGemmSquare>::CW;
+  const size_t lds = gemm_lds(ga.nbk, sh).total;
+  const int64_t gx = (ga.Nc + CW - 1) / CW, gy = (ga.M + RW - 1) / RW;
   if (lds > 160 * 1024 || gy > 65535) return MXA_ERR_UNSUPPORTED;
   if (ga.bpd && batch == 1 && ga.nbk <= kGemmDigNbkMax) {
     // a prepared weight: the exponent-folded digits, every row block in the one launch (a
@@ -30,9 +37,12 @@ static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, hipStream_t stream)
     hipLaunchKernelGGL(mx_gemm_dig_kernel<PLAIN>, dim3((unsigned)((ga.M + 31) / 32)), dim3(256), dl, stream, ga);
     return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
   }
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return MXA_ERR_LAUNCH;
+  // (the wide strip stages float32 rows: only the PLAIN instantiation has it)
+  constexpr int kWide = PLAIN ? kGemmWide : kGemmSquare;
+  const void* gk = sh == kGemmTall   ? reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN, kGemmTall>)
+                   : sh == kGemmWide ? reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN, kWide>)
+                                     : reinterpret_cast<const void*>(&mx_gemm_kernel<PLAIN, kGemmSquare>);
+  if (hipFuncSetAttribute(gk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return MXA_ERR_LAUNCH;
   // grid.z <= 65535: larger batches in slices; a wave whose spreads the int32 sums cannot
   // take sums its blocks in fp64 itself (gemm_tile's run_f64): one launch per slice
   const int64_t esz = (ga.linear || ga.dt == kF32) ? 4 : 2;
@@ -41,7 +51,10 @@ static int launch_gemm_p(const GemmArgs& ga0, int64_t batch, hipStream_t stream)
     gs.a += b0 * ga.a_bat; gs.ae += b0 * ga.ae_bat; gs.b += b0 * ga.b_bat; gs.be += b0 * ga.be_bat;
     gs.c = static_cast<unsigned char*>(ga.c) + b0 * ga.c_bat * esz;
     const int64_t nb = std::min<int64_t>(65535, batch - b0);
-    hipLaunchKernelGGL(mx_gemm_kernel<PLAIN>, dim3((unsigned)gx, (unsigned)gy, (unsigned)nb), dim3(256), lds, stream, gs);
+    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)nb);
+    if (sh == kGemmTall) hipLaunchKernelGGL((mx_gemm_kernel<PLAIN, kGemmTall>), grid, dim3(256), lds, stream, gs);
+    else if (sh == kGemmWide) hipLaunchKernelGGL((mx_gemm_kernel<PLAIN, kWide>), grid, dim3(256), lds, stream, gs);
+    else hipLaunchKernelGGL((mx_gemm_kernel<PLAIN, kGemmSquare>), grid, dim3(256), lds, stream, gs);
     if (hipGetLastError() != hipSuccess) return MXA_ERR_LAUNCH;
   }
   return MXA_OK;

@@ -29,32 +29,50 @@
 namespace mxa {
 
 constexpr int kGemmRows = 64, kGemmCols = 128;
+// Tile shapes (four waves of 32 rows x 64 columns each):
+//   kGemmSquare  64 x 128, waves 2 x 2 (the general case, the Linear)
+//   kGemmTall    128 x 64, waves 4 x 1: products of <= 64 columns (the drop-in's P.V: the
+//                64 x 128 tile would leave half its waves without columns)
+//   kGemmWide    32 x 256, waves 1 x 4: float32 products of 65..256 contiguous columns (the
+//                drop-in's QK^T, 197 x 197 per head): a 32-row strip of whole output rows, staged
+//                in LDS and written as one contiguous run (rows of 197 floats are not 16-B
+//                aligned: per-lane column stores touched two lines per 128-B segment)
+constexpr int kGemmSquare = 0, kGemmTall = 1, kGemmWide = 2;
+template <int SH>
+struct GemmShape {
+  static constexpr int RW = SH == kGemmTall ? 128 : SH == kGemmWide ? 32 : kGemmRows;
+  static constexpr int CW = SH == kGemmTall ? 64 : SH == kGemmWide ? 256 : kGemmCols;
+  static constexpr int RPT = 256 / RW, CPT = 256 / CW;  // prologue threads per row / column
+};
 
 struct GemmLds {
-  size_t xe, ce, rlo, rn, clo, cn, rhi, chi, part, total;
+  size_t xe, ce, rlo, rn, clo, cn, rhi, chi, part, stage, total;
 };
-__host__ __device__ inline GemmLds gemm_lds(int nbk) {
+__host__ __device__ inline GemmLds gemm_lds(int nbk, int sh) {
   GemmLds L;
   size_t o = 0;
-  L.xe = o;  // row exponent offsets [nbk][64] int16
-  o += (size_t)nbk * kGemmRows * 2;
-  L.ce = o;  // column exponent offsets [nbk][128] int16
-  o += (size_t)nbk * kGemmCols * 2;
+  // (per-row arrays of 128, per-column arrays of 256: any tile shape)
+  L.xe = o;  // row exponent offsets [nbk][RW] int16
+  o += (size_t)nbk * 128 * 2;
+  L.ce = o;  // column exponent offsets [nbk][CW] int16
+  o += (size_t)nbk * 256 * 2;
   o = (o + 15) & ~(size_t)15;
   L.rlo = o;
-  o += kGemmRows * 4;
+  o += 128 * 4;
   L.rn = o;
-  o += kGemmRows * 4;
+  o += 128 * 4;
   L.clo = o;
-  o += kGemmCols * 4;
+  o += 256 * 4;
   L.cn = o;
-  o += kGemmCols * 4;
+  o += 256 * 4;
   L.rhi = o;
-  o += kGemmRows * 4;
+  o += 128 * 4;
   L.chi = o;
-  o += kGemmCols * 4;
+  o += 256 * 4;
   L.part = o;  // prologue partials [3][256]
   o += 3 * 256 * 4;
+  L.stage = o;  // kGemmWide: the strip's float32 output rows [32][Nc <= 256]
+  if (sh == kGemmWide) o += 32 * 256 * 4;
   L.total = o;
   return L;
 }
@@ -63,12 +81,15 @@ __host__ __device__ inline GemmLds gemm_lds(int nbk) {
 // (run_f64: no list, no follow-up kernel).
 // PLAIN: float32 output, no bfloat / autocast rounding (the bench and workload settings):
 // the epilogue is a store (+ bias), compiled without the general rounding code.
-template <bool PLAIN>
+template <bool PLAIN, int SH>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm, int tn, unsigned char* smem) {
+  using S = GemmShape<SH>;
+  constexpr bool kStage = SH == kGemmWide;  // (PLAIN, one column tile, ldc == Nc: the launcher)
+  constexpr int RW = S::RW, CW = S::CW, RPT = S::RPT, CPT = S::CPT;
   typedef int v16i_g __attribute__((ext_vector_type(16)));
   typedef int v4i_g __attribute__((ext_vector_type(4)));
   const int nbk = a.nbk;
-  const GemmLds L = gemm_lds(nbk);
+  const GemmLds L = gemm_lds(nbk, SH);
   int16_t* xe = reinterpret_cast<int16_t*>(smem + L.xe);
   int16_t* ce = reinterpret_cast<int16_t*>(smem + L.ce);
   int* rlo = reinterpret_cast<int*>(smem + L.rlo);
@@ -76,7 +97,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   int* clo = reinterpret_cast<int*>(smem + L.clo);
   int* cn = reinterpret_cast<int*>(smem + L.cn);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int m0g = tm * kGemmRows, n0g = tn * kGemmCols;
+  const int m0g = tm * RW, n0g = tn * CW;
   const int16_t* aeb = a.ae + bat * a.ae_bat;
   const int16_t* beb = a.be + bat * a.be_bat;
 
@@ -97,7 +118,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     const uint4 u = *reinterpret_cast<const uint4*>(p), v = *reinterpret_cast<const uint4*>(p + hoff);
     return ((u.x | u.y | u.z | u.w) | (v.x | v.y | v.z | v.w)) == 0u;
   };
-  // Per row 4 threads and per column 2 threads reduce strided K-block subsets (consecutive
+  // Per row RPT threads and per column CPT threads reduce strided K-block subsets (consecutive
   // threads on consecutive exponents: coalesced, independent loads), partials through LDS.
   int* chi = reinterpret_cast<int*>(smem + L.chi);
   int* rhi_ = reinterpret_cast<int*>(smem + L.rhi);
@@ -115,24 +136,24 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
         hi = max(hi, e);
       }
     };
-    // rows: thread (r = tid / 4, q = tid % 4) takes K-blocks q, q + 4, ...
+    // rows: thread (r = tid / RPT, q = tid % RPT) takes K-blocks q, q + RPT, ...
     {
-      const int r = tid >> 2, q = tid & 3;
+      const int r = tid / RPT, q = tid % RPT;
       if (m0g + r < a.M)
-        for (int kb = q; kb < nbk; kb += 4) take(true, r, kb, a_exp(r, kb));
+        for (int kb = q; kb < nbk; kb += RPT) take(true, r, kb, a_exp(r, kb));
     }
     part[tid] = lo;
     part[256 + tid] = hi;
     part[512 + tid] = nan;
   }
   __syncthreads();
-  if (tid < kGemmRows) {
+  if (tid < RW) {
     int lo = 1 << 20, hi = -(1 << 20), nan = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      lo = min(lo, part[4 * tid + q]);
-      hi = max(hi, part[256 + 4 * tid + q]);
-      nan |= part[512 + 4 * tid + q];
+    for (int q = 0; q < RPT; ++q) {
+      lo = min(lo, part[RPT * tid + q]);
+      hi = max(hi, part[256 + RPT * tid + q]);
+      nan |= part[512 + RPT * tid + q];
     }
     if (lo > hi) lo = hi = 0;
     rlo[tid] = lo;
@@ -142,11 +163,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
   __syncthreads();
   {
     int lo = 1 << 20, hi = -(1 << 20), nan = 0;
-    // columns: [kb][n] exponents -- thread (c = tid % 128, half = tid / 128) takes K-blocks
-    // half, half + 2, ...; [n][kb] -- thread (c = tid / 2, half = tid % 2)
-    const int c = bk_major ? (tid & 127) : (tid >> 1), h = bk_major ? (tid >> 7) : (tid & 1);
+    // columns: [kb][n] exponents -- thread (c = tid % CW, h = tid / CW) takes K-blocks
+    // h, h + CPT, ...; [n][kb] -- thread (c = tid / CPT, h = tid % CPT)
+    const int c = bk_major ? (tid % CW) : (tid / CPT), h = bk_major ? (tid / CW) : (tid % CPT);
     if (n0g + c < a.Nc)
-      for (int kb = h; kb < nbk; kb += 2) {
+      for (int kb = h; kb < nbk; kb += CPT) {
         const int e = b_exp(c, kb);
         if (e == kExpNaN) {
           nan = 1;
@@ -160,29 +181,37 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     part[512 + tid] = nan;
   }
   __syncthreads();
-  if (tid < kGemmCols) {
-    const int t0 = bk_major ? tid : 2 * tid, t1 = bk_major ? tid + 128 : 2 * tid + 1;
-    int lo = min(part[t0], part[t1]), hi = max(part[256 + t0], part[256 + t1]);
+  if (tid < CW) {
+    int lo = 1 << 20, hi = -(1 << 20), nan = 0;
+#pragma unroll
+    for (int h = 0; h < CPT; ++h) {
+      const int t = bk_major ? tid + CW * h : CPT * tid + h;
+      lo = min(lo, part[t]);
+      hi = max(hi, part[256 + t]);
+      nan |= part[512 + t];
+    }
     if (lo > hi) lo = hi = 0;
     clo[tid] = lo;
     chi[tid] = hi;
-    cn[tid] = part[512 + t0] | part[512 + t1];
+    cn[tid] = nan;
   }
   __syncthreads();
-  for (int i = tid; i < nbk * kGemmRows; i += 256) {
-    const int kb = i / kGemmRows, r = i - kb * kGemmRows;
+  for (int i = tid; i < nbk * RW; i += 256) {
+    const int kb = i / RW, r = i - kb * RW;
     const int e = m0g + r < a.M ? a_exp(r, kb) : 0;
     xe[i] = (int16_t)(e == kExpNaN || zero_blk(true, r, kb, e) ? 0 : e - rlo[r]);
   }
-  for (int i = tid; i < nbk * kGemmCols; i += 256) {
-    const int kb = i / kGemmCols, c = i - kb * kGemmCols;
+  for (int i = tid; i < nbk * CW; i += 256) {
+    const int kb = i / CW, c = i - kb * CW;
     const int e = n0g + c < a.Nc ? b_exp(c, kb) : 0;
     ce[i] = (int16_t)(e == kExpNaN || zero_blk(false, c, kb, e) ? 0 : e - clo[c]);
   }
   __syncthreads();
 
   // ---- this wave: rows wr0 .. +31, columns wc0 .. +63 of the tile ------------------
-  const int wr0 = 32 * (wave & 1), wc0 = 64 * (wave >> 1);
+  const int wr0 = SH == kGemmTall ? 32 * wave : SH == kGemmWide ? 0 : 32 * (wave & 1);
+  const int wc0 = SH == kGemmTall ? 0 : SH == kGemmWide ? 64 * wave : 64 * (wave >> 1);
+  float* stage = reinterpret_cast<float*>(smem + L.stage);
   const int ln = lane & 31, kh = 16 * (lane >> 5), m0 = 4 * (lane >> 5);
   // the wave's fast-path test: its rows' largest spread + its columns' largest spread,
   // and the smallest output scale (a subnormal result would round twice)
@@ -238,7 +267,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3), lc = wc0 + 32 * j + ln;
     if (rn[lr] || cn[lc]) o = __uint_as_float(0x7FC00000u);
     const int64_t off = bat * a.c_bat + (int64_t)m * a.ldc + n;
-    if constexpr (PLAIN) {
+    if constexpr (kStage) {
+      stage[lr * a.Nc + n] = a.bias ? o + a.bias[n] : o;
+    } else if constexpr (PLAIN) {
       static_cast<float*>(a.c)[off] = a.bias ? o + a.bias[n] : o;
     } else if (a.linear) {
       // autocast: F.linear returns the dtype, then the output rounding (linear.py:88-92),
@@ -262,11 +293,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
       for (int i = 0; i < 16; ++i) acc[i] = 0.0;
       for (int kb = 0; kb < nbk; ++kb) {
         const v16i_g c = __builtin_amdgcn_mfma_i32_32x32x32_i8(ld(ap, kb), ldb(bp, kb), zero, 0, 0, 0);
-        const int dc = xcol[kb * kGemmCols + 32 * j] + lc;
+        const int dc = xcol[kb * CW + 32 * j] + lc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int lr = wr0 + 8 * (i >> 2) + m0 + (i & 3);
-          acc[i] += ldexp((double)c[i], xe[kb * kGemmRows + lr] + rlo[lr] + dc);
+          acc[i] += ldexp((double)c[i], xe[kb * RW + lr] + rlo[lr] + dc);
         }
       }
 #pragma unroll
@@ -281,10 +312,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
     for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0;
     // block kb's shifted sums: row offset (4 rows per uint2 read) + column offset
     auto epi = [&](const v16i_g& c0, const v16i_g& c1, int kb) {
-      const int d0 = xcol[kb * kGemmCols], d1 = xcol[kb * kGemmCols + 32];
+      const int d0 = xcol[kb * CW], d1 = xcol[kb * CW + 32];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint2 e4 = *reinterpret_cast<const uint2*>(xrow + kb * kGemmRows + 8 * q);
+        const uint2 e4 = *reinterpret_cast<const uint2*>(xrow + kb * RW + 8 * q);
         const int dx[4] = {(int)(int16_t)(e4.x & 0xFFFFu), (int)(int16_t)(e4.x >> 16), (int)(int16_t)(e4.y & 0xFFFFu),
                            (int)(int16_t)(e4.y >> 16)};
 #pragma unroll
@@ -327,13 +358,27 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int64_t bat, int tm
       store(1, i, ldexpf((float)acc1[i], lr + lc1));
     }
   }
+  if constexpr (kStage) {  // the strip's rows, contiguous in the output: 16-B stores
+    typedef float f32x4_a4g __attribute__((ext_vector_type(4), aligned(4)));
+    __syncthreads();
+    const int n = min(RW, a.M - m0g) * a.Nc;
+    float* dst = static_cast<float*>(a.c) + bat * a.c_bat + (int64_t)m0g * a.Nc;
+    for (int i = 4 * tid; i < n; i += 4 * 256) {
+      if (i + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(stage + i);
+        *reinterpret_cast<f32x4_a4g*>(dst + i) = f32x4_a4g{v.x, v.y, v.z, v.w};
+      } else {
+        for (int t = i; t < n; ++t) dst[t] = stage[t];
+      }
+    }
+  }
 }
 
 // (3 waves per SIMD: 166 VGPRs without spills; a cap of 4 spills ~640 registers)
-template <bool PLAIN>
+template <bool PLAIN, int SH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void mx_gemm_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemm_tile<PLAIN>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
+  gemm_tile<PLAIN, SH>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
 }
 
 // ---- exponent-folded digits (mx.Linear with a prepared weight) ----------------------

@@ -118,14 +118,18 @@ __global__ __launch_bounds__(256) void bfloat_kernel(const void* __restrict__ x,
 // 8 lanes per 32-element block, 4 floats (16 B) per lane (body: mxa_prep.hpp)
 // ---------------------------------------------------------------------------
 // 16 consecutive elements of a row (from element c0) of storage dtype DT as floats
+// (float32: 16-B loads at any 4-B alignment -- rows of a length that is not a multiple of 4,
+// such as the drop-in's 197-key P rows, take global_load_dwordx4 too: gfx950 executes
+// dword-aligned 16-B global loads; the vector type states the 4-B alignment)
+typedef float f32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <int DT>
 __device__ __forceinline__ void load_row16(const void* xr, int c0, int D, bool vec, bool valid, float xv[16]) {
   if constexpr (DT == kF32) {
     const float* x = static_cast<const float*>(xr);
-    if (valid && vec && c0 + 16 <= D) {
+    if (valid && c0 + 16 <= D) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(x + c0 + 4 * q);
+        const f32x4_a4 v = *reinterpret_cast<const f32x4_a4*>(x + c0 + 4 * q);
         xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
       }
     } else {

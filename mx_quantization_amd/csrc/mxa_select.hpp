@@ -629,9 +629,22 @@ __device__ __forceinline__ bool topk_rows16(const GrpTopkArgs& a, const TopkWs& 
   const GrpRow<El> g = carve_grp<El>(smem + (size_t)(4 * wave + gi) * grp_row_bytes(npa, NP, sizeof(El)), npa, NP);
   const int64_t src = (valid ? row : 0) * a.ld;
   uint32_t bad = 0u;
-  if (valid)
-    for (int j = gl; j < a.n; j += 16) {
-      const float v = load_dt(a.vals, src + j, a.dt);
+  // the row's values, 256 (64-bit elements: 128) at a time: every load of a chunk issued before
+  // the first is used (one load at a time left each wave waiting out a memory round trip per 16
+  // values)
+  constexpr int kChunk = NP < (kPacked ? 256 : 128) ? NP : (kPacked ? 256 : 128);
+  for (int c0 = 0; c0 < NP; c0 += kChunk) {
+    float vv[kChunk / 16];
+#pragma unroll
+    for (int t = 0; t < kChunk / 16; ++t) {
+      const int j = c0 + gl + 16 * t;
+      vv[t] = valid && j < a.n ? load_dt(a.vals, src + j, a.dt) : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < kChunk / 16; ++t) {
+      const int j = c0 + gl + 16 * t;
+      if (!valid || j >= a.n) continue;
+      const float v = vv[t];
       if constexpr (kPacked) {
         bad |= q_bad_bits(v);
         if (a.out_vals) bad |= q_val_bad(v);  // the tail rebuilds the values from the elements
@@ -640,6 +653,7 @@ __device__ __forceinline__ bool topk_rows16(const GrpTopkArgs& a, const TopkWs& 
         g.A[j] = pack_ki(order_key(v), (uint32_t)j);
       }
     }
+  }
   bool left = false;
   if constexpr (kPacked) {
     const uint64_t bw = __builtin_amdgcn_ballot_w64(bad != 0u);
