@@ -29,9 +29,9 @@ static int launch_select_w(const Rows2Args& ra0, int BH, hipStream_t stream, boo
   ra.rows_per_wg = sel_rows_per_wg(BH, ra.N);
   const unsigned gy = (unsigned)((ra.N + ra.rows_per_wg - 1) / ra.rows_per_wg);
   dim3 grid((unsigned)BH, gy);
-  if (sizeof(El) == 8 && ra.fb_only) {  // one workgroup per 64 flags of the packed pass
+  if (sizeof(El) == 8 && ra.fb_only) {  // one workgroup per kFbItems flags of the packed pass
     ra.fb_gy = (int)gy;
-    grid = dim3((unsigned)(((int64_t)BH * gy + 63) / 64), 1);
+    grid = dim3((unsigned)(((int64_t)BH * gy + kFbItems - 1) / kFbItems), 1);
   }
   hipLaunchKernelGGL((select_kernel<NP, MODE, W, El, QM, TW>), grid, dim3(64 * W), lds, stream, ra);
   return hipGetLastError() == hipSuccess ? MXA_OK : MXA_ERR_LAUNCH;
@@ -161,7 +161,7 @@ static int launch_topk_packed(const GrpTopkArgs& ga, const TopkWs& w, unsigned g
   }
   TopkWs f = w;
   f.fb_only = 1;
-  return launch_topk_grp<NP>(ga, f, (unsigned)((w.n_wg + 63) / 64), stream);
+  return launch_topk_grp<NP>(ga, f, (unsigned)((w.n_wg + kFbItems - 1) / kFbItems), stream);
 }
 
 static int topk_check(const void* vals, int64_t rows, int32_t n, int64_t ld, int32_t k, int64_t* out_idx, int32_t dtype) {

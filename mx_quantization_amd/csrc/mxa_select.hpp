@@ -31,6 +31,10 @@
 namespace mxa {
 
 constexpr int kSelRows = 32;   // query rows per workgroup (a multiple of 4 * waves)
+// packed-pass workgroup flags per 64-bit-pass workgroup: few, so that a call whose rows mostly
+// do not pack still spreads the 64-bit pass over the chip (64 per workgroup ran arbitrary float32
+// rows through ops.topk at half the rate of the 64-bit pass alone: 1.60 vs 0.80 ms, round 6)
+constexpr int kFbItems = 4;
 #ifndef MXA_SEL_OCC
 #define MXA_SEL_OCC 4  // (a tools-only build of another occupancy target for same-box A/Bs)
 #endif
@@ -562,7 +566,7 @@ __device__ __forceinline__ bool select_item(const Rows2Args& a, unsigned char* s
 // Selection kernel, four query rows per wave.  El = uint64_t: rows of up to 512 keys,
 // every approximator.  El = uint32_t: the packed pass (rows of <= 256 keys; half the LDS
 // per row, so more resident waves); each workgroup flags (a.fb_flags[bh * gy + y]) whether
-// it left rows for the 64-bit pass, which then runs with fb_only: one workgroup per 64
+// it left rows for the 64-bit pass, which then runs with fb_only: one workgroup per kFbItems
 // flags, taking the flagged items one after another (a call without such rows costs a
 // small grid that exits at once).
 template <int NP, int MODE, int kSelWaves, typename El = uint64_t, int QM = 0, int TW = 0>
@@ -571,8 +575,8 @@ __global__ __launch_bounds__(64 * kSelWaves) __attribute__((amdgpu_waves_per_eu(
   if (sizeof(El) == 8 && a.fb_only) {
     __shared__ uint64_t sbits;
     const int gy = a.fb_gy;
-    const int64_t items = (int64_t)a.B * a.H * gy, i0 = (int64_t)blockIdx.x * 64;
-    if (threadIdx.x < 64) {
+    const int64_t items = (int64_t)a.B * a.H * gy, i0 = (int64_t)blockIdx.x * kFbItems;
+    if (threadIdx.x < kFbItems) {
       const bool f = i0 + threadIdx.x < items && a.fb_flags[i0 + threadIdx.x] != 0u;
       const uint64_t bits = __builtin_amdgcn_ballot_w64(f);
       if (threadIdx.x == 0) sbits = bits;
@@ -702,15 +706,15 @@ __device__ __forceinline__ bool topk_rows16(const GrpTopkArgs& a, const TopkWs& 
   return __syncthreads_or(left ? 1 : 0) != 0;
 }
 
-// El = uint64_t: every row (w.fb_only: one workgroup per 64 flags of the packed pass, taking
+// El = uint64_t: every row (w.fb_only: one workgroup per kFbItems flags of the packed pass, taking
 // the flagged workgroups' left rows); El = uint32_t: the packed pass, flagging per workgroup
 template <int NP, typename El = uint64_t, int QM = 0, int TW = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(El) == 4 ? 5 : NP <= 256 ? 4 : 2, 8))) void topk_grp_kernel(GrpTopkArgs a, TopkWs w) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (sizeof(El) == 8 && w.fb_only) {
     __shared__ uint64_t sbits;
-    const int64_t i0 = (int64_t)blockIdx.x * 64;
-    if (threadIdx.x < 64) {
+    const int64_t i0 = (int64_t)blockIdx.x * kFbItems;
+    if (threadIdx.x < kFbItems) {
       const bool f = i0 + threadIdx.x < w.n_wg && w.fb_flags[i0 + threadIdx.x] != 0u;
       const uint64_t bits = __builtin_amdgcn_ballot_w64(f);
       if (threadIdx.x == 0) sbits = bits;

@@ -133,10 +133,16 @@ def approx_values(X: torch.Tensor, kind: str, flush: bool = False, bfloat: int =
     return out
 
 
-def topk(vals: torch.Tensor, k: int, return_mask: bool = False):
+def topk(vals: torch.Tensor, k: int, return_mask: bool = False, packed: bool = True):
     """torch.topk(vals, k, dim=-1, largest=True, sorted=True) with torch's CPU
     index order (TopKImpl.h:45-86), computed on the device.  Returns (values, idx),
-    plus the prune mask as packed words (..., ceil(n/32)) int32 if return_mask."""
+    plus the prune mask as packed words (..., ceil(n/32)) int32 if return_mask.
+
+    packed (rows of <= 256 values): try the packed 32-bit pass first (mxa_topk_ws) -- the
+    fast path for approximate scores, whose values leave the low mantissa byte free; rows
+    that do not pack are redone by the 64-bit pass.  For arbitrary float rows (almost none
+    pack) packed=False runs the 64-bit pass alone: DeiT-base-sized random rows 0.79 ms
+    against 1.05 ms through the packed attempt (profiles/r06v1_ab_topk_fp32.txt)."""
     dev = require_device(vals)
     dt = _dt(vals, "vals")
     vals = vals.contiguous()
@@ -148,13 +154,17 @@ def topk(vals: torch.Tensor, k: int, return_mask: bool = False):
     if rows:
         # the workspace path (rows of <= 256 values: the fused op's packed selection pass
         # and one-lane tail); 0 bytes: mxa_topk alone
+        mp = mask.data_ptr() if return_mask else None
+        if not packed:  # the 64-bit pass alone
+            check(lib().mxa_topk(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(), mp, dt,
+                                 stream_ptr(dev)), "mxa_topk")
+            return (out, idx, mask) if return_mask else (out, idx)
         wsb = lib().mxa_topk_workspace_bytes(rows, n, k)
         if wsb < 0:
             raise ValueError(f"topk: invalid shape rows={rows} n={n} k={k}")
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-        check(lib().mxa_topk_ws(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(),
-                                mask.data_ptr() if return_mask else None, dt, ws.data_ptr(), wsb,
-                                stream_ptr(dev)), "mxa_topk")
+        check(lib().mxa_topk_ws(vals.data_ptr(), rows, n, n, k, idx.data_ptr(), out.data_ptr(), mp, dt, ws.data_ptr(),
+                                wsb, stream_ptr(dev)), "mxa_topk")
     return (out, idx, mask) if return_mask else (out, idx)
 
 

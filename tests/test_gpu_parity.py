@@ -159,6 +159,8 @@ def test_topk_random_small_alphabets_and_specials(M):
             _, want = O.topk(rows, k)
             _, idx = M.topk(dev(rows), k)
             same(host(idx), want, f"n{n} k{k}")
+            _, idx = M.topk(dev(rows), k, packed=False)  # the 64-bit pass alone
+            same(host(idx), want, f"n{n} k{k} unpacked")
 
 
 def test_topk_prune_mask_words(M):
@@ -167,9 +169,10 @@ def test_topk_prune_mask_words(M):
     for name in ("deit", "dit", "cross"):
         k = int(d[f"{name}_k"])
         pred = d[f"{name}_pred"]
-        _, idx, words = M.topk(dev(pred), k, return_mask=True)
         n = pred.shape[-1]
-        same(host(M.unpack_mask(words, n)), O.prune_mask(d[f"{name}_idx"].astype(np.int64), n), name)
+        for packed in (True, False):
+            _, idx, words = M.topk(dev(pred), k, return_mask=True, packed=packed)
+            same(host(M.unpack_mask(words, n)), O.prune_mask(d[f"{name}_idx"].astype(np.int64), n), f"{name} {packed}")
 
 
 @pytest.mark.parametrize("n", [33, 64, 65, 100, 197, 256, 512])
