@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MXA_ABI_VERSION 5
+#define MXA_ABI_VERSION 6  /* 6: mxa_matmul_bt */
 
 /* status codes */
 #define MXA_OK 0

@@ -21,7 +21,7 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 MXA_OK = 0
 MXA_OP_SIGN, MXA_OP_MXINT8, MXA_OP_MXINT4, MXA_OP_EXION, MXA_OP_TRUE_EX = range(5)
-ABI_VERSION = 5
+ABI_VERSION = 6
 DT_F32, DT_F16, DT_BF16 = 0, 1, 2
 DTYPES = {torch.float32: DT_F32, torch.float16: DT_F16, torch.bfloat16: DT_BF16}
 PATH_NAMES = {2: "rows_fused", 3: "rows_split"}  # mxa_attention_path

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(N.EXPORTS), "ctypes signatures out of sync with include/mxa.h"
-    assert lib.mxa_abi_version() == N.ABI_VERSION == 5
+    assert lib.mxa_abi_version() == N.ABI_VERSION == 6
 
 
 def test_status_strings_and_arg_errors():
