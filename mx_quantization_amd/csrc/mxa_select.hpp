@@ -35,18 +35,13 @@ constexpr int kSelRows = 32;   // query rows per workgroup (a multiple of 4 * wa
 // do not pack still spreads the 64-bit pass over the chip (64 per workgroup ran arbitrary float32
 // rows through ops.topk at half the rate of the 64-bit pass alone: 1.60 vs 0.80 ms, round 6)
 constexpr int kFbItems = 4;
-#ifndef MXA_SEL_OCC
-#define MXA_SEL_OCC 4  // (a tools-only build of another occupancy target for same-box A/Bs)
-#endif
-constexpr int kSelOcc = MXA_SEL_OCC;  // waves per SIMD the 64-bit pass is compiled for (rows <= 256 keys)
-#ifndef MXA_SEL_POCC
-#define MXA_SEL_POCC 5  // (a tools-only build of another occupancy target for same-box A/Bs)
-#endif
-constexpr int kSelPOcc = MXA_SEL_POCC;  // ... and the packed pass
-#ifndef MXA_SEL_POCC_NT
-#define MXA_SEL_POCC_NT 5
-#endif
-constexpr int kSelPOccNT = MXA_SEL_POCC_NT;  // ... the packed pass without the tail (k > 33: DiT)
+// waves per SIMD the 64-bit pass is compiled for (rows <= 256 keys; 6 / 8 measured slower at
+// PixArt's rows: spills, profiles/r06_ab_tail.txt)
+constexpr int kSelOcc = 4;
+// ... and the packed pass, with the tail (DeiT: 6 measured slower, spills) and without it
+// (k > 33, DiT: 4 removes its spills and measured slower) -- profiles/r06_ab_tail.txt
+constexpr int kSelPOcc = 5;
+constexpr int kSelPOccNT = 5;
 constexpr int kSelShortT = 224;
 // waves per workgroup: 2 for rows of <= 224 keys on a large grid (DeiT-base: 0.97 ->
 // 0.93 ms), else 4 (DiT: 1.44 vs 1.56 ms with 2; PixArt's 128 heads: 0.069 vs 0.10 ms)
@@ -366,10 +361,7 @@ __device__ __forceinline__ void sel_scores(const Rows2Args& a, const SelTabs& t,
           sink(j, v, key, std::true_type{});
         }
       };
-#ifndef MXA_SEL_KUNROLL
-#define MXA_SEL_KUNROLL 1  // (tools-only builds of other unroll factors for same-box A/Bs)
-#endif
-#pragma unroll MXA_SEL_KUNROLL
+#pragma unroll 1  // (unrolled by 2 / 4: the same within the spread, profiles/r06_ab_tail.txt)
       for (int i = 0; i < nt - 1; ++i) one(i, std::false_type{});
       one(nt - 1, std::true_type{});
       if (__builtin_amdgcn_ballot_w64(redo != 0u) != 0) {  // rare: the exact path for those keys
