@@ -46,7 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MXINT8 attn fwd tokens/s/GPU (DeiT-base, DiT-XL/2); top-k idx bit-match"
-PROFILE_TAG = "r06v1"  # the profiling session whose committed PMC files the bench line cites
+PROFILE_TAG = "r06v2"  # the profiling session whose committed PMC files the bench line cites
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: dense I8 MFMA = 2x BF16 (~2.5 PF) per clock
 
